@@ -1,0 +1,690 @@
+// ge_fa.hip -- single-level ForceAtlas on gfx950.
+//
+// Reference: partition::forceAtlas, include/forceatlas.hpp:89-305.
+//
+// One iteration = two kernels on the context stream:
+//   fa_repulse_*        O(n^2) all-pairs repulsion for rows [rb,re)       (:151-167)
+//                       -> Frep (per-row partial force, fp64)
+//   fa_attract_update_* CSR attraction continuing each row's sum (:169-203),
+//                       gravity (:205-211), swing (:214-217), speed clamp and
+//                       position update (:246-261) -> X_next rows, Fprev rows
+// The global swing/traction sums of :219-244 are dead (overwritten with 1.0 at
+// :228, :242) and are not computed.
+//
+// STRICT mode (default) keeps the reference's serial op order per row: the
+// j loop is ascending over all vertices, the CSR walk is in stored order, every
+// multiply/add/div/sqrt rounds separately (-ffp-contract=off, IEEE div/sqrt).
+// Each thread owns R rows and streams the coordinates of all j through LDS
+// tiles, so a row's sum is exactly the reference's sum.  Two exact rewrites:
+//   * -(x_j - x_i) is computed as (x_i - x_j).  They differ only in the sign of
+//     a zero, and a zero contribution never changes a running force sum: the
+//     sum starts at +0.0 and IEEE round-to-nearest never produces -0.0 from a
+//     sum unless both addends are -0.0.  For the same reason the j == i term
+//     (direction 0/eps = 0) is accumulated instead of branched around.
+//   * 0.0 + t*t (the first term of distance(), :72-75) is t*t.
+//
+// FAST mode re-associates: 2-D tiles over (row block, j block) partial sums,
+// FMA, one reciprocal square root per pair.  Checked against strict within
+// 1e-5 relative after the iteration counts the reference runs (tests).
+//
+// Small graphs (n <= 1024, e.g. the coarsest level, 1e5 iterations) run all
+// iterations inside one workgroup with coordinates resident in LDS.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "ge_internal.hpp"
+
+namespace ge {
+namespace {
+
+constexpr double kEps = 0.00001;  // include/forceatlas.hpp:110
+
+struct FaConst {
+  double ks_gS;    // ks * globalSpeed (globalSpeed = tolerate * 1.0 / 1.0)
+  double gS;       // globalSpeed
+  double ksmax, repel, attract, gravity, delta;
+  int use_weights, linlog, nohubs;
+};
+
+FaConst make_const(const ge_fa_params& p) {
+  FaConst c;
+  c.gS = p.tolerate * 1.0 / 1.0;  // :244 with :228, :242
+  c.ks_gS = p.ks * c.gS;
+  c.ksmax = p.ksmax;
+  c.repel = p.repel;
+  c.attract = p.attract;
+  c.gravity = p.gravity;
+  c.delta = p.delta;
+  c.use_weights = p.use_weights;
+  c.linlog = p.linlog;
+  c.nohubs = p.nohubs;
+  return c;
+}
+
+__device__ __forceinline__ double clamp_eps(double x) { return x < kEps ? kEps : x; }
+
+// Attraction magnitude, include/forceatlas.hpp:176-196.  The linlog / delta != 1
+// branches call device log/pow (ocml), which may differ from glibc in the last
+// ulp: only the default branch is bit-exact.
+__device__ __forceinline__ double attraction_mag(double dis, double a, double dip1,
+                                                 const FaConst& c) {
+  double f = dis;
+  if (c.linlog) f = log(1 + f);
+  if (c.delta == 1.0) {
+    f = f * a;
+  } else if (c.delta != 0.0) {
+    double sgn = (a < 0) ? -1.0 : 1.0;
+    double mg = (a < 0) ? -a : a;
+    f = sgn * pow(mg, c.delta) * f;
+  }
+  if (c.nohubs) f = f / dip1;
+  return c.attract * f;
+}
+
+// deg[i] + 1 with deg the serial row sum of include/forceatlas.hpp:127-140.
+__global__ void degp1_kernel(int n, const int* __restrict__ ip, const double* __restrict__ dx,
+                             int use_weights, double* __restrict__ dp1) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double d;
+  if (use_weights) {
+    d = 0.0;
+    for (int e = ip[i]; e < ip[i + 1]; ++e) d += dx[e];
+  } else {
+    d = 1.0 * (ip[i + 1] - ip[i]);
+  }
+  dp1[i] = d + 1;
+}
+
+// ---------------------------------------------------------------------------
+// STRICT repulsion.  Block = 256 threads, each owns R rows (stride 256), the j
+// range is streamed through an LDS tile of 256 records {x_0..x_{D-1}, deg+1}.
+
+constexpr int kRepThreads = 256;
+constexpr int kTileJ = 256;
+
+template <int D>
+struct Rec {
+  static constexpr int W = (D + 1 <= 4) ? 4 : 8;  // doubles per LDS record
+};
+
+template <int D, int R, bool REPEL_ONE>
+__global__ void __launch_bounds__(kRepThreads)
+fa_repulse_strict(int n, int rb, int re, const double* __restrict__ X,
+                  const double* __restrict__ dp1, double repel, double* __restrict__ Frep) {
+  constexpr int W = Rec<D>::W;
+  __shared__ __attribute__((aligned(16))) double tile[kTileJ * W];
+  const int tid = threadIdx.x;
+  const int base = rb + blockIdx.x * (kRepThreads * R);
+
+  double xi[R][D], di[R], acc[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = base + tid + r * kRepThreads;
+    const bool ok = i < re;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xi[r][k] = ok ? X[(size_t)i * D + k] : 0.0;
+      acc[r][k] = 0.0;
+    }
+    di[r] = ok ? dp1[i] : 1.0;
+  }
+
+  for (int j0 = 0; j0 < n; j0 += kTileJ) {
+    const int cnt = min(kTileJ, n - j0);
+    __syncthreads();
+    if (tid < cnt) {
+      const int j = j0 + tid;
+#pragma unroll
+      for (int k = 0; k < D; ++k) tile[tid * W + k] = X[(size_t)j * D + k];
+      tile[tid * W + D] = dp1[j];
+    }
+    __syncthreads();
+    for (int jj = 0; jj < cnt; ++jj) {
+      double xj[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) xj[k] = tile[jj * W + k];
+      const double dj = tile[jj * W + D];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        double e[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) e[k] = xi[r][k] - xj[k];
+        double s = e[0] * e[0];
+#pragma unroll
+        for (int k = 1; k < D; ++k) s = s + e[k] * e[k];
+        const double dis = clamp_eps(sqrt(s));
+        double cij = di[r] * dj;
+        if (!REPEL_ONE) cij = cij * repel;
+        const double val = cij / (dis * dis);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + (e[k] / dis) * val;
+      }
+    }
+  }
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = base + tid + r * kRepThreads;
+    if (i < re) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) Frep[(size_t)(i - rb) * D + k] = acc[r][k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FAST repulsion: (row block) x (j block) tiles; each block writes a partial
+// sum for its rows into Fpart[jb][row]; fa_reduce_parts sums the partials.
+// Pair term in closed form: F_i += c_ij * (x_i - x_j) / dis^3, dis from one
+// rsqrt + one Newton step, FMA everywhere.
+
+constexpr int kFastJBlocks = 16;  // j-range split
+
+template <int D, int R>
+__global__ void __launch_bounds__(kRepThreads)
+fa_repulse_fast(int n, int rb, int re, const double* __restrict__ X,
+                const double* __restrict__ dp1, double repel, int jblocks,
+                double* __restrict__ Fpart) {
+  constexpr int W = Rec<D>::W;
+  __shared__ __attribute__((aligned(16))) double tile[kTileJ * W];
+  const int tid = threadIdx.x;
+  const int rows_here = re - rb;
+  const int base = rb + blockIdx.x * (kRepThreads * R);
+  const int jb = blockIdx.y;
+  const int jchunk = (n + jblocks - 1) / jblocks;
+  const int jbeg = jb * jchunk;
+  const int jend = min(n, jbeg + jchunk);
+  const double inv_eps = 1.0 / kEps;
+
+  double xi[R][D], di[R], acc[R][D];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = base + tid + r * kRepThreads;
+    const bool ok = i < re;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xi[r][k] = ok ? X[(size_t)i * D + k] : 0.0;
+      acc[r][k] = 0.0;
+    }
+    di[r] = (ok ? dp1[i] : 1.0) * repel;
+  }
+  for (int j0 = jbeg; j0 < jend; j0 += kTileJ) {
+    const int cnt = min(kTileJ, jend - j0);
+    __syncthreads();
+    if (tid < cnt) {
+      const int j = j0 + tid;
+#pragma unroll
+      for (int k = 0; k < D; ++k) tile[tid * W + k] = X[(size_t)j * D + k];
+      tile[tid * W + D] = dp1[j];
+    }
+    __syncthreads();
+    for (int jj = 0; jj < cnt; ++jj) {
+      double xj[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) xj[k] = tile[jj * W + k];
+      const double dj = tile[jj * W + D];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        double e[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) e[k] = xi[r][k] - xj[k];
+        double s = e[0] * e[0];
+#pragma unroll
+        for (int k = 1; k < D; ++k) s = fma(e[k], e[k], s);
+        // y = 1/max(sqrt(s), eps): hardware estimate + two Newton steps.
+        // s == 0 gives inf -> NaN after Newton -> fmin picks 1/eps.
+        double y = __builtin_amdgcn_rsq(s);
+        const double hs = 0.5 * s;
+        y = y * fma(-hs * y, y, 1.5);
+        y = y * fma(-hs * y, y, 1.5);
+        y = fmin(y, inv_eps);
+        const double w = di[r] * dj * (y * y * y);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[r][k] = fma(e[k], w, acc[r][k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int i = base + tid + r * kRepThreads;
+    if (i < re) {
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        Fpart[((size_t)jb * rows_here + (i - rb)) * D + k] = acc[r][k];
+    }
+  }
+}
+
+template <int D>
+__global__ void fa_reduce_parts(int rows, int jblocks, const double* __restrict__ Fpart,
+                                double* __restrict__ Frep) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * D) return;
+  double s = 0.0;
+  for (int b = 0; b < jblocks; ++b) s += Fpart[(size_t)b * rows * D + t];
+  Frep[t] = s;
+}
+
+// ---------------------------------------------------------------------------
+// Attraction + gravity + swing + update, one thread per row (serial CSR order).
+
+template <int D>
+__device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D], double (&acc)[D],
+                                           double dip1, const FaConst& c,
+                                           double* __restrict__ Fprev,
+                                           double* __restrict__ Xnext) {
+  double m2 = xi[0] * xi[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
+  const double mag = sqrt(m2);  // not clamped (:205)
+  double F[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double unit = -xi[k] / mag;
+    const double g = unit * c.gravity * dip1;
+    F[k] = acc[k] + g;
+  }
+  double s = 0.0, f2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    const double t = Fprev[(size_t)li * D + k] - F[k];
+    s = (k == 0) ? t * t : s + t * t;
+    f2 = (k == 0) ? F[k] * F[k] : f2 + F[k] * F[k];
+  }
+  const double swing = sqrt(s);  // not clamped in single-level (:216)
+  const double totalF = sqrt(f2);
+  double speed = c.ks_gS / (1 + c.gS * sqrt(swing));
+  const double cap = c.ksmax / totalF;
+  if (speed > cap) speed = cap;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    Xnext[(size_t)i * D + k] = F[k] * speed + xi[k];
+    Fprev[(size_t)li * D + k] = F[k];
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(256)
+fa_attract_update_strict(int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
+                         const double* __restrict__ dx, const double* __restrict__ X,
+                         const double* __restrict__ dp1, const double* __restrict__ Frep,
+                         double* __restrict__ Fprev, double* __restrict__ Xnext, FaConst c) {
+  const int i = rb + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= re) return;
+  const int li = i - rb;
+  double xi[D], acc[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xi[k] = X[(size_t)i * D + k];
+    acc[k] = Frep[(size_t)li * D + k];
+  }
+  const double dip1 = dp1[i];
+  const int e1 = ip[i + 1];
+  for (int e = ip[i]; e < e1; ++e) {
+    const int j = ix[e];
+    double t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) t[k] = X[(size_t)j * D + k] - xi[k];
+    double s = t[0] * t[0];
+#pragma unroll
+    for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
+    const double dis = clamp_eps(sqrt(s));
+    const double a = c.use_weights ? dx[e] : 1.0;
+    const double Fa = attraction_mag(dis, a, dip1, c);
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+  }
+  finish_row<D>(i, li, xi, acc, dip1, c, Fprev, Xnext);
+}
+
+// ---------------------------------------------------------------------------
+// Small graphs: one workgroup runs every iteration, coordinates in LDS.
+
+constexpr int kSmallMax = 1024;
+
+template <int D>
+__global__ void __launch_bounds__(256)
+fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
+                const double* __restrict__ dx, const double* __restrict__ dp1g,
+                double* __restrict__ Xg, int iterations, FaConst c) {
+  constexpr int W = Rec<D>::W;
+  constexpr int RM = kSmallMax / 256;
+  __shared__ __attribute__((aligned(16))) double sx[kSmallMax * W];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += 256) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) sx[i * W + k] = Xg[(size_t)i * D + k];
+    sx[i * W + D] = dp1g[i];
+  }
+  double fprev[RM][D], F[RM][D];
+#pragma unroll
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int k = 0; k < D; ++k) fprev[r][k] = 0.0;
+
+  for (int it = 0; it < iterations; ++it) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = tid + r * 256;
+      if (i >= n) break;
+      double xi[D], acc[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        xi[k] = sx[i * W + k];
+        acc[k] = 0.0;
+      }
+      const double dip1 = sx[i * W + D];
+      for (int j = 0; j < n; ++j) {
+        double e[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) e[k] = xi[k] - sx[j * W + k];
+        double s = e[0] * e[0];
+#pragma unroll
+        for (int k = 1; k < D; ++k) s = s + e[k] * e[k];
+        const double dis = clamp_eps(sqrt(s));
+        double cij = dip1 * sx[j * W + D];
+        cij = cij * c.repel;
+        const double val = cij / (dis * dis);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+      }
+      for (int e = ip[i]; e < ip[i + 1]; ++e) {
+        const int j = ix[e];
+        double t[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = sx[j * W + k] - xi[k];
+        double s = t[0] * t[0];
+#pragma unroll
+        for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
+        const double dis = clamp_eps(sqrt(s));
+        const double a = c.use_weights ? dx[e] : 1.0;
+        const double Fa = attraction_mag(dis, a, dip1, c);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+      }
+      double m2 = xi[0] * xi[0];
+#pragma unroll
+      for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
+      const double mag = sqrt(m2);
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double unit = -xi[k] / mag;
+        F[r][k] = acc[k] + unit * c.gravity * dip1;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int i = tid + r * 256;
+      if (i >= n) break;
+      double s = 0.0, f2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double t = fprev[r][k] - F[r][k];
+        s = (k == 0) ? t * t : s + t * t;
+        f2 = (k == 0) ? F[r][k] * F[r][k] : f2 + F[r][k] * F[r][k];
+      }
+      const double swing = sqrt(s);
+      const double totalF = sqrt(f2);
+      double speed = c.ks_gS / (1 + c.gS * sqrt(swing));
+      const double cap = c.ksmax / totalF;
+      if (speed > cap) speed = cap;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        sx[i * W + k] = F[r][k] * speed + sx[i * W + k];
+        fprev[r][k] = F[r][k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += 256)
+#pragma unroll
+    for (int k = 0; k < D; ++k) Xg[(size_t)i * D + k] = sx[i * W + k];
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch helpers
+
+constexpr int kRowsPerThread = 4;  // strict repulsion: 1024 rows per block
+constexpr int kRowsPerThreadFast = 4;
+
+template <int D>
+void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const double* X,
+                      const double* dp1, double repel, double* Frep, double* Fpart) {
+  const int rows = re - rb;
+  if (rows <= 0) return;
+  if (mode == GE_MODE_FAST) {
+    const int per = kRepThreads * kRowsPerThreadFast;
+    const int jb = std::max(1, std::min(kFastJBlocks, (n + kTileJ - 1) / kTileJ));
+    dim3 grid((rows + per - 1) / per, jb);
+    hipLaunchKernelGGL((fa_repulse_fast<D, kRowsPerThreadFast>), grid, dim3(kRepThreads), 0, s,
+                       n, rb, re, X, dp1, repel, jb, Fpart);
+    const int tot = rows * D;
+    hipLaunchKernelGGL((fa_reduce_parts<D>), dim3((tot + 255) / 256), dim3(256), 0, s, rows, jb,
+                       Fpart, Frep);
+    return;
+  }
+  const int per = kRepThreads * kRowsPerThread;
+  dim3 grid((rows + per - 1) / per);
+  if (repel == 1.0)
+    hipLaunchKernelGGL((fa_repulse_strict<D, kRowsPerThread, true>), grid, dim3(kRepThreads), 0,
+                       s, n, rb, re, X, dp1, repel, Frep);
+  else
+    hipLaunchKernelGGL((fa_repulse_strict<D, kRowsPerThread, false>), grid, dim3(kRepThreads),
+                       0, s, n, rb, re, X, dp1, repel, Frep);
+}
+
+template <int D>
+void launch_attract(hipStream_t s, int rb, int re, const int* ip, const int* ix,
+                    const double* dx, const double* X, const double* dp1, const double* Frep,
+                    double* Fprev, double* Xnext, const FaConst& c) {
+  const int rows = re - rb;
+  if (rows <= 0) return;
+  hipLaunchKernelGGL((fa_attract_update_strict<D>), dim3((rows + 255) / 256), dim3(256), 0, s,
+                     rb, re, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c);
+}
+
+template <class F>
+void dispatch_dim(int dim, F&& f) {
+  switch (dim) {
+    case 1: f(std::integral_constant<int, 1>()); break;
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    case 4: f(std::integral_constant<int, 4>()); break;
+    default: throw Error(GE_ERR_ARG, "dimension must be 1..4");
+  }
+}
+
+}  // namespace
+}  // namespace ge
+
+// ---------------------------------------------------------------------------
+// plan
+
+struct ge_fa_plan {
+  ge_ctx* ctx = nullptr;
+  int n = 0, nnz = 0, dim = 0, rb = 0, re = 0;
+  const int* ip = nullptr;
+  const int* ix = nullptr;
+  const double* dx = nullptr;
+  ge_fa_params p{};
+  ge::FaConst c{};
+  ge::DevBuf<double> dp1, frep, fprev, fpart;
+  bool profiling = false;
+  std::vector<hipEvent_t> events;  // 3 per timed step
+  size_t next_event = 0;
+};
+
+namespace ge {
+
+static void plan_init(ge_fa_plan* pl) {
+  const int rows = pl->re - pl->rb;
+  pl->dp1.alloc(pl->n);
+  pl->frep.alloc((size_t)std::max(rows, 1) * pl->dim);
+  pl->fprev.alloc((size_t)std::max(rows, 1) * pl->dim);
+  if (pl->p.mode == GE_MODE_FAST)
+    pl->fpart.alloc((size_t)std::max(rows, 1) * pl->dim * kFastJBlocks);
+  hipStream_t s = pl->ctx->stream;
+  hipLaunchKernelGGL(degp1_kernel, dim3((pl->n + 255) / 256), dim3(256), 0, s, pl->n, pl->ip,
+                     pl->dx, pl->p.use_weights, pl->dp1.p);
+  GE_HIP(hipGetLastError());
+  GE_HIP(hipMemsetAsync(pl->fprev.p, 0, sizeof(double) * pl->fprev.n, s));
+}
+
+static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
+  hipStream_t s = pl->ctx->stream;
+  hipEvent_t* ev = nullptr;
+  if (pl->profiling) {
+    if (pl->next_event + 3 > pl->events.size()) {
+      for (int k = 0; k < 3 * 64; ++k) {
+        hipEvent_t e;
+        GE_HIP(hipEventCreate(&e));
+        pl->events.push_back(e);
+      }
+    }
+    ev = &pl->events[pl->next_event];
+    pl->next_event += 3;
+    GE_HIP(hipEventRecord(ev[0], s));
+  }
+  dispatch_dim(pl->dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
+                        pl->frep.p, pl->fpart.p);
+    if (ev) GE_HIP(hipEventRecord(ev[1], s));
+    launch_attract<D>(s, pl->rb, pl->re, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
+                      pl->fprev.p, xn, pl->c);
+  });
+  GE_HIP(hipGetLastError());
+  if (ev) GE_HIP(hipEventRecord(ev[2], s));
+}
+
+void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
+                   const double* d_dx, int dim, double* d_x, int iterations,
+                   const ge_fa_params& p) {
+  if (n <= 0 || iterations <= 0) return;
+  hipStream_t s = ctx->stream;
+  if (n <= kSmallMax && p.mode == GE_MODE_STRICT) {
+    DevBuf<double> dp1(n);
+    hipLaunchKernelGGL(degp1_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, d_ip, d_dx,
+                       p.use_weights, dp1.p);
+    FaConst c = make_const(p);
+    dispatch_dim(dim, [&](auto Dc) {
+      constexpr int D = decltype(Dc)::value;
+      hipLaunchKernelGGL((fa_small_strict<D>), dim3(1), dim3(256), 0, s, n, d_ip, d_ix, d_dx,
+                         dp1.p, d_x, iterations, c);
+    });
+    GE_HIP(hipGetLastError());
+    GE_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  ge_fa_plan pl;
+  pl.ctx = ctx;
+  pl.n = n;
+  pl.nnz = nnz;
+  pl.dim = dim;
+  pl.rb = 0;
+  pl.re = n;
+  pl.ip = d_ip;
+  pl.ix = d_ix;
+  pl.dx = d_dx;
+  pl.p = p;
+  pl.c = make_const(p);
+  plan_init(&pl);
+  DevBuf<double> other((size_t)n * dim);
+  double* cur = d_x;
+  double* nxt = other.p;
+  for (int it = 0; it < iterations; ++it) {
+    plan_step(&pl, cur, nxt);
+    std::swap(cur, nxt);
+  }
+  if (cur != d_x)
+    GE_HIP(hipMemcpyAsync(d_x, cur, sizeof(double) * n * dim, hipMemcpyDeviceToDevice, s));
+  GE_HIP(hipStreamSynchronize(s));
+}
+
+}  // namespace ge
+
+extern "C" {
+
+int ge_fa_plan_create(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
+                      const double* d_dx, int dim, const ge_fa_params* p, int rb, int re,
+                      ge_fa_plan** out) {
+  return ge::guarded([&] {
+    GE_REQUIRE(ctx && p && out, "null argument");
+    GE_REQUIRE(n > 0 && dim >= 1 && dim <= 4, "bad n or dim (dim must be 1..4)");
+    GE_REQUIRE(0 <= rb && rb <= re && re <= n, "bad row range");
+    ge::DeviceGuard g(ctx);
+    auto* pl = new ge_fa_plan();
+    pl->ctx = ctx;
+    pl->n = n;
+    pl->nnz = nnz;
+    pl->dim = dim;
+    pl->rb = rb;
+    pl->re = re;
+    pl->ip = d_ip;
+    pl->ix = d_ix;
+    pl->dx = d_dx;
+    pl->p = *p;
+    pl->c = ge::make_const(*p);
+    try {
+      ge::plan_init(pl);
+    } catch (...) {
+      delete pl;
+      throw;
+    }
+    *out = pl;
+  });
+}
+
+int ge_fa_plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && xc && xn && xc != xn, "bad plan step arguments");
+    ge::DeviceGuard g(pl->ctx);
+    ge::plan_step(pl, xc, xn);
+  });
+}
+
+int ge_fa_plan_set_profiling(ge_fa_plan* pl, int enable) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl, "null plan");
+    pl->profiling = enable != 0;
+    pl->next_event = 0;
+  });
+}
+
+int ge_fa_plan_kernel_ms(ge_fa_plan* pl, double* rep_ms, double* attr_ms, int* launches) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && rep_ms && attr_ms && launches, "null argument");
+    ge::DeviceGuard g(pl->ctx);
+    GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+    double a = 0.0, b = 0.0;
+    int cnt = 0;
+    for (size_t k = 0; k + 3 <= pl->next_event; k += 3) {
+      float t1 = 0.f, t2 = 0.f;
+      GE_HIP(hipEventElapsedTime(&t1, pl->events[k], pl->events[k + 1]));
+      GE_HIP(hipEventElapsedTime(&t2, pl->events[k + 1], pl->events[k + 2]));
+      a += t1;
+      b += t2;
+      ++cnt;
+    }
+    *rep_ms = cnt ? a / cnt : 0.0;
+    *attr_ms = cnt ? b / cnt : 0.0;
+    *launches = cnt;
+  });
+}
+
+int ge_fa_plan_destroy(ge_fa_plan* pl) {
+  return ge::guarded([&] {
+    if (!pl) return;
+    for (hipEvent_t e : pl->events) (void)hipEventDestroy(e);
+    delete pl;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,384 @@
+"""ctypes binding of libge.so (include/ge.h) -- the host-side mirror of
+graph-embed's partition:: API for Python callers, tests and the benchmark.
+
+The library is the product: every call below runs the gfx950 HIP kernels (or,
+for the host-resident steps, the library's own C++).  There is no CPU fallback:
+if libge.so is missing or no device is visible, the device entry points raise.
+
+Reference interfaces mirrored (LLNL/graph-embed):
+  force_atlas        partition::forceAtlas          include/forceatlas.hpp:89-312
+  force_atlas_ml     partition::forceAtlasMultilevel include/forceatlas.hpp:314-574
+  partition          partition::partition (hierarchy) src/partitioner.cpp:1550-1893
+  interpolation_matrix                               src/partitioner.cpp:29-65
+  ptap               P_T.Mult(A).Mult(P_T.Transpose()) examples/embed.cpp:96-98
+  embed              partition::embed                src/embed.cpp:561-796
+  modularity         partition::modularity           src/partitioner.cpp:69-114
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libge.so")
+HEADER = os.path.join(REPO_ROOT, "include", "ge.h")
+
+MODE_STRICT = 0
+MODE_FAST = 1
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_vp = ctypes.c_void_p
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+class GeError(RuntimeError):
+    pass
+
+
+class FaParams(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_double) for k in
+                ("ks", "ksmax", "repel", "attract", "gravity", "delta", "tolerate")] + \
+               [(k, ctypes.c_int) for k in ("use_weights", "linlog", "nohubs", "normalize")] + \
+               [("seed", ctypes.c_uint), ("mode", ctypes.c_int)]
+
+
+_SIGS = {
+    "ge_fa_params_default": (None, [ctypes.POINTER(FaParams)]),
+    "ge_last_error": (ctypes.c_char_p, []),
+    "ge_version": (ctypes.c_char_p, []),
+    "ge_device_count": (ctypes.c_int, [_ip]),
+    "ge_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ge_ctx_destroy": (ctypes.c_int, [_vp]),
+    "ge_ctx_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "ge_ctx_sync": (ctypes.c_int, [_vp]),
+    "ge_force_atlas": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                      _f64p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(FaParams)]),
+    "ge_fa_plan_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp,
+                                         ctypes.c_int, ctypes.POINTER(FaParams), ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ge_fa_plan_step": (ctypes.c_int, [_vp, _vp, _vp]),
+    "ge_fa_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "ge_fa_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double), _ip]),
+    "ge_fa_plan_destroy": (ctypes.c_int, [_vp]),
+    "ge_force_atlas_ml": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                         _i32p, _i32p, _i32p, _f64p, _f64p, _f64p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(FaParams)]),
+    "ge_partition": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_double,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                    ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ge_hier_levels": (ctypes.c_int, [_vp, _ip]),
+    "ge_hier_shape": (ctypes.c_int, [_vp, ctypes.c_int, _ip, _ip]),
+    "ge_hier_copy": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p]),
+    "ge_hier_free": (ctypes.c_int, [_vp]),
+    "ge_interpolation_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                               ctypes.POINTER(_vp)]),
+    "ge_ptap": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _i32p,
+                               _i32p, ctypes.POINTER(_vp)]),
+    "ge_csr_shape": (ctypes.c_int, [_vp, _ip, _ip, ctypes.POINTER(ctypes.c_longlong)]),
+    "ge_csr_copy": (ctypes.c_int, [_vp, _i32p, _vp, _vp]),
+    "ge_csr_free": (ctypes.c_int, [_vp]),
+    "ge_modularity": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _i32p,
+                                     ctypes.POINTER(ctypes.c_double)]),
+    "ge_embed": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _i32p, _f64p,
+                                _i32p, _i32p, _i32p, _i32p, _i32p, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(FaParams), _f64p]),
+    "ge_radius_step": (ctypes.c_int, [ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "ge_uniform_stream": (ctypes.c_int, [ctypes.c_uint, ctypes.c_longlong, _f64p]),
+    "ge_rmat_csr": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                   ctypes.POINTER(_vp)]),
+    "ge_largest_component": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p,
+                                            ctypes.POINTER(_vp)]),
+}
+
+_lib = None
+
+
+def build():
+    """Compile libge.so in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.check_call(["make", "-s", "-C", PKG_ROOT, "-j8"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GeError(f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
+                          "(no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        msg = lib().ge_last_error().decode(errors="replace")
+        raise GeError(f"libge error {rc}: {msg}")
+
+
+def params(**kw):
+    p = FaParams()
+    lib().ge_fa_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise TypeError(f"unknown ForceAtlas parameter {k}")
+        setattr(p, k, v)
+    return p
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    _check(lib().ge_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def _csr(A):
+    ip, ix, dx = A
+    return (np.ascontiguousarray(ip, dtype=np.int32), np.ascontiguousarray(ix, dtype=np.int32),
+            np.ascontiguousarray(dx, dtype=np.float64))
+
+
+class Context:
+    """One device + one HIP stream (ge_ctx)."""
+
+    def __init__(self, device=0):
+        h = _vp()
+        _check(lib().ge_ctx_create(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().ge_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr):
+        _check(lib().ge_ctx_set_stream(self.h, _vp(stream_ptr) if stream_ptr else None))
+
+    def sync(self):
+        _check(lib().ge_ctx_sync(self.h))
+
+    # -- ForceAtlas ----------------------------------------------------------
+    def force_atlas(self, A, dim, coords=None, iterations=100000, **kw):
+        ip, ix, dx = _csr(A)
+        n = len(ip) - 1
+        X = np.zeros((n, dim)) if coords is None else np.array(coords, dtype=np.float64)
+        X = np.ascontiguousarray(X)
+        p = params(**kw)
+        _check(lib().ge_force_atlas(self.h, n, ip, ix, dx, dim, X.reshape(-1),
+                                    int(coords is None), iterations, ctypes.byref(p)))
+        return X
+
+    def force_atlas_ml(self, A, PT, vertex_A, coords_A, r_A, dim, iterations=10, **kw):
+        ip, ix, dx = _csr(A)
+        pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+        pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+        n = len(ip) - 1
+        X = np.zeros((n, dim))
+        p = params(**kw)
+        _check(lib().ge_force_atlas_ml(
+            self.h, n, ip, ix, dx, len(pip) - 1, pip, pix,
+            np.ascontiguousarray(vertex_A, dtype=np.int32),
+            np.ascontiguousarray(coords_A, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(r_A, dtype=np.float64), X.reshape(-1), dim, iterations,
+            ctypes.byref(p)))
+        return X
+
+    def ptap(self, A, PT):
+        ip, ix, dx = _csr(A)
+        pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+        pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+        h = _vp()
+        _check(lib().ge_ptap(self.h, len(ip) - 1, ip, ix, dx, len(pip) - 1, pip, pix,
+                             ctypes.byref(h)))
+        return _take_csr(h)
+
+    def embed(self, As, hier, dim, base_iterations=100000, ml_iterations=100,
+              print_progress=False, **kw):
+        parts = concat_levels(As, hier)
+        out = np.empty((len(As[0][0]) - 1, dim))
+        p = params(**kw)
+        _check(lib().ge_embed(self.h, len(hier), *parts, dim, base_iterations, ml_iterations,
+                              int(print_progress), ctypes.byref(p), out.reshape(-1)))
+        return out
+
+    def fa_plan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw):
+        return FaPlan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw)
+
+
+class FaPlan:
+    """Device-resident ForceAtlas iteration over rows [row_begin, row_end)
+    (ge_fa_plan_*).  Device pointers are raw integers (e.g. tensor.data_ptr())."""
+
+    def __init__(self, ctx, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw):
+        self.ctx = ctx
+        p = params(**kw)
+        h = _vp()
+        _check(lib().ge_fa_plan_create(ctx.h, n, nnz, _vp(d_ip), _vp(d_ix), _vp(d_dx), dim,
+                                       ctypes.byref(p), row_begin, row_end, ctypes.byref(h)))
+        self.h = h
+
+    def step(self, d_x_cur, d_x_next):
+        _check(lib().ge_fa_plan_step(self.h, _vp(d_x_cur), _vp(d_x_next)))
+
+    def set_profiling(self, on):
+        _check(lib().ge_fa_plan_set_profiling(self.h, int(on)))
+
+    def kernel_ms(self):
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _check(lib().ge_fa_plan_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b),
+                                          ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def close(self):
+        if self.h:
+            lib().ge_fa_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _take_csr(h):
+    r, c, z = ctypes.c_int(), ctypes.c_int(), ctypes.c_longlong()
+    _check(lib().ge_csr_shape(h, ctypes.byref(r), ctypes.byref(c), ctypes.byref(z)))
+    ip = np.empty(r.value + 1, dtype=np.int32)
+    ix = np.empty(z.value, dtype=np.int32)
+    dx = np.empty(z.value, dtype=np.float64)
+    _check(lib().ge_csr_copy(h, ip, ix.ctypes.data_as(_vp), dx.ctypes.data_as(_vp)))
+    lib().ge_csr_free(h)
+    return ip, ix, dx
+
+
+# -- host-resident entry points (no device needed) ----------------------------
+
+def partition(A, coarsening_factor, printing=False, positive_merging=True, stall=1.0,
+              matching_iterations=2, merge_leaves=False):
+    """Hierarchy of P_T matrices as (indptr, indices, rows, cols) tuples."""
+    ip, ix, dx = _csr(A)
+    h = _vp()
+    _check(lib().ge_partition(None, len(ip) - 1, ip, ix, dx, coarsening_factor, int(printing),
+                              int(positive_merging), stall, matching_iterations,
+                              int(merge_leaves), ctypes.byref(h)))
+    try:
+        lv = ctypes.c_int()
+        _check(lib().ge_hier_levels(h, ctypes.byref(lv)))
+        out = []
+        for l in range(lv.value):
+            r, c = ctypes.c_int(), ctypes.c_int()
+            _check(lib().ge_hier_shape(h, l, ctypes.byref(r), ctypes.byref(c)))
+            pip = np.empty(r.value + 1, dtype=np.int32)
+            pix = np.empty(c.value, dtype=np.int32)
+            _check(lib().ge_hier_copy(h, l, pip, pix))
+            out.append((pip, pix, r.value, c.value))
+        return out
+    finally:
+        lib().ge_hier_free(h)
+
+
+def interpolation_matrix(num_cols, sets):
+    offs = np.zeros(len(sets) + 1, dtype=np.int32)
+    offs[1:] = np.cumsum([len(s) for s in sets])
+    flat = np.ascontiguousarray(np.concatenate([np.asarray(s, dtype=np.int32) for s in sets])
+                                if sets else np.zeros(0, np.int32), dtype=np.int32)
+    h = _vp()
+    _check(lib().ge_interpolation_matrix(num_cols, len(sets), offs, flat, ctypes.byref(h)))
+    return _take_csr(h)
+
+
+def modularity(A, vertex_A, m):
+    ip, ix, dx = _csr(A)
+    q = ctypes.c_double()
+    _check(lib().ge_modularity(len(ip) - 1, ip, ix, dx, m,
+                               np.ascontiguousarray(vertex_A, dtype=np.int32), ctypes.byref(q)))
+    return q.value
+
+
+def radius_step(coords_A, dim, coarse_is_base, PTc=None, coords_Ac=None, r_Ac=None, Ac=None):
+    """Returns (r_A, coords_A after the rescale)."""
+    cA = np.array(coords_A, dtype=np.float64, copy=True).reshape(-1)
+    m = cA.size // dim
+    rA = np.zeros(m)
+    keep = []
+
+    def ptr(a, dt):
+        if a is None:
+            return None
+        a = np.ascontiguousarray(a, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data_as(_vp)
+
+    mc = 0 if PTc is None else len(PTc[0]) - 1
+    _check(lib().ge_radius_step(
+        m, cA, rA, dim, int(coarse_is_base), mc,
+        ptr(None if PTc is None else PTc[0], np.int32), ptr(None if PTc is None else PTc[1], np.int32),
+        ptr(coords_Ac, np.float64), ptr(r_Ac, np.float64),
+        ptr(None if Ac is None else Ac[0], np.int32), ptr(None if Ac is None else Ac[1], np.int32)))
+    return rA, cA.reshape(m, dim)
+
+
+def uniform_stream(seed, count):
+    out = np.empty(count, dtype=np.float64)
+    _check(lib().ge_uniform_stream(seed, count, out))
+    return out
+
+
+def rmat_csr(n, draws, seed=12345):
+    h = _vp()
+    _check(lib().ge_rmat_csr(n, draws, seed, ctypes.byref(h)))
+    return _take_csr(h)
+
+
+def largest_component(A):
+    ip, ix, dx = _csr(A)
+    h = _vp()
+    _check(lib().ge_largest_component(len(ip) - 1, ip, ix, dx, ctypes.byref(h)))
+    return _take_csr(h)
+
+
+def vertex_of(PT):
+    pip, pix = np.asarray(PT[0]), np.asarray(PT[1])
+    v = np.empty(len(pix), dtype=np.int32)
+    sizes = np.diff(pip)
+    v[pix] = np.repeat(np.arange(len(sizes), dtype=np.int32), sizes)
+    return v
+
+
+def concat_levels(As, hier):
+    a_n = np.array([len(a[0]) - 1 for a in As], dtype=np.int32)
+    a_off = np.cumsum([0] + [len(a[0]) for a in As])[:-1].astype(np.int32)
+    a_nz = np.cumsum([0] + [len(a[1]) for a in As])[:-1].astype(np.int32)
+    a_ip = np.concatenate([np.asarray(a[0]) for a in As]).astype(np.int32)
+    a_ix = np.concatenate([np.asarray(a[1]) for a in As]).astype(np.int32)
+    a_dx = np.concatenate([np.asarray(a[2]) for a in As]).astype(np.float64)
+    p_rows = np.array([p[2] for p in hier] + [0], dtype=np.int32)
+    p_off = np.cumsum([0] + [len(p[0]) for p in hier]).astype(np.int32)
+    p_nz = np.cumsum([0] + [len(p[1]) for p in hier]).astype(np.int32)
+    p_ip = np.concatenate([np.asarray(p[0]) for p in hier] + [np.zeros(1)]).astype(np.int32)
+    p_ix = np.concatenate([np.asarray(p[1]) for p in hier] + [np.zeros(1)]).astype(np.int32)
+    return a_n, a_off, a_nz, a_ip, a_ix, a_dx, p_rows, p_off, p_nz, p_ip, p_ix
+
+
+def header_symbols():
+    """Function names declared in include/ge.h."""
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ge_\w+)\s*\(", txt, re.M)))

@@ -1,0 +1,175 @@
+/*
+ * ge.h -- C ABI of libge.so, the MI355X-native (gfx950) implementation of
+ * graph-embed's hot path: multilevel modularity coarsening + ForceAtlas.
+ *
+ * Plain C: pointers and sizes only, no C++ or torch types.  Every function
+ * returns 0 on success or a non-zero GE_ERR_* / HIP error code; the text of the
+ * last error on the calling thread is ge_last_error().  (The reference reports
+ * errors only through assert; the drop-in headers in graph-embed_amd/include turn a non-zero
+ * status into std::runtime_error.)
+ *
+ * Memory: functions named *_plan_* and ge_fa_plan_step take DEVICE pointers
+ * (data resident in HBM); every other entry point takes HOST pointers and moves
+ * the data itself.  All device work is enqueued on the context's stream.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to LLNL/graph-embed).
+ */
+#ifndef GE_H
+#define GE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GE_OK 0
+#define GE_ERR_ARG 1001     /* invalid argument / shape mismatch */
+#define GE_ERR_HIP 1002     /* a HIP runtime call failed */
+#define GE_ERR_STATE 1003   /* object used in the wrong state */
+#define GE_ERR_NOMEM 1004   /* host allocation failed */
+
+#define GE_MODE_STRICT 0 /* bit-exact with the reference's serial op order */
+#define GE_MODE_FAST 1   /* re-associated / FMA / rsqrt; 1e-5 relative bar */
+
+typedef struct ge_ctx ge_ctx;
+typedef struct ge_hier ge_hier;
+typedef struct ge_csr ge_csr;
+typedef struct ge_fa_plan ge_fa_plan;
+
+/* ForceAtlas parameters.  Defaults (ge_fa_params_default) are those of
+ * forceAtlas / forceAtlasMultilevel, include/forceatlas.hpp:89-103, :320-331. */
+typedef struct ge_fa_params {
+  double ks, ksmax, repel, attract, gravity, delta, tolerate;
+  int use_weights, linlog, nohubs, normalize;
+  unsigned seed; /* mt19937 seed replacing std::random_device (:104-105, :332-333) */
+  int mode;      /* GE_MODE_STRICT (default) or GE_MODE_FAST */
+} ge_fa_params;
+
+void ge_fa_params_default(ge_fa_params* p);
+const char* ge_last_error(void);
+const char* ge_version(void);
+
+/* ---- context: one device + one stream; reentrant, no global mutable state ---- */
+int ge_device_count(int* count);
+int ge_ctx_create(int device, ge_ctx** out);
+int ge_ctx_destroy(ge_ctx* ctx);
+/* Enqueue on an external hipStream_t (e.g. torch's current stream); NULL
+ * restores the context's own stream. */
+int ge_ctx_set_stream(ge_ctx* ctx, void* hip_stream);
+int ge_ctx_sync(ge_ctx* ctx);
+
+/* ---- single-level ForceAtlas ----
+ * Replaces partition::forceAtlas(A, dim, coords, iterations, ks, ksmax, repel,
+ * attract, gravity, useWeights, linlog, nohubs, delta, tolerate, normalize)
+ * (include/forceatlas.hpp:89-305) and, with init_random = 1 and
+ * iterations = 100000, partition::forceAtlas(A, dim) (:307-312).
+ * coords: n*dim row-major, in/out.  init_random != 0 draws U(-1,1) from
+ * mt19937(p->seed) in the reference order (:118-125). */
+int ge_force_atlas(ge_ctx* ctx, int n, const int* indptr, const int* indices,
+                   const double* data, int dim, double* coords, int init_random,
+                   int iterations, const ge_fa_params* p);
+
+/* Device-resident ForceAtlas iteration over rows [row_begin, row_end) -- the
+ * loop body of include/forceatlas.hpp:146-270 -- for row-sharded multi-GPU use.
+ * The plan keeps d_indptr/d_indices/d_data by pointer (caller owns them). */
+int ge_fa_plan_create(ge_ctx* ctx, int n, int nnz, const int* d_indptr,
+                      const int* d_indices, const double* d_data, int dim,
+                      const ge_fa_params* p, int row_begin, int row_end,
+                      ge_fa_plan** out);
+/* d_x_cur: all n*dim coordinates of this iteration; writes rows
+ * [row_begin,row_end) of d_x_next (must not alias d_x_cur). */
+int ge_fa_plan_step(ge_fa_plan* plan, const double* d_x_cur, double* d_x_next);
+/* Kernel timing with HIP events on the plan's stream (0 = off). */
+int ge_fa_plan_set_profiling(ge_fa_plan* plan, int enable);
+/* Average device ms per launch of the repulsion and attraction/update kernels
+ * since profiling was enabled; *launches = steps timed. Synchronises. */
+int ge_fa_plan_kernel_ms(ge_fa_plan* plan, double* repulsion_ms, double* attraction_ms,
+                         int* launches);
+int ge_fa_plan_destroy(ge_fa_plan* plan);
+
+/* ---- multilevel ForceAtlas ----
+ * Replaces partition::forceAtlasMultilevel(A, P, v_A, coords_A, r_A, coords,
+ * dim, iterations, ks, ksmax, useWeights, linlog, nohubs, repel, attract,
+ * gravity, delta, tolerate) (include/forceatlas.hpp:314-574), in the reference's
+ * single-thread random draw order.  m = P_T rows; coords: n*dim out. */
+int ge_force_atlas_ml(ge_ctx* ctx, int n, const int* indptr, const int* indices,
+                      const double* data, int m, const int* pt_indptr,
+                      const int* pt_indices, const int* vertex_A, const double* coords_A,
+                      const double* r_A, double* coords, int dim, int iterations,
+                      const ge_fa_params* p);
+
+/* ---- coarsening hierarchy ----
+ * Replaces std::vector<SparseMatrix> partition::partition(A, coarseningFactor,
+ * printing, positiveMerging, stallStopThreshold, matchingIterations,
+ * mergeLeaves) (include/partitioner.hpp:52-53, src/partitioner.cpp:1550-1893).
+ * A must be symmetric.  Level l of the result is P_T[l] (rows x cols, one 1.0
+ * per column). */
+int ge_partition(ge_ctx* ctx, int n, const int* indptr, const int* indices,
+                 const double* data, double coarsening_factor, int printing,
+                 int positive_merging, double stall_stop_threshold,
+                 int matching_iterations, int merge_leaves, ge_hier** out);
+int ge_hier_levels(const ge_hier* h, int* levels);
+int ge_hier_shape(const ge_hier* h, int level, int* rows, int* cols);
+/* indptr: rows+1 ints, indices: cols ints */
+int ge_hier_copy(const ge_hier* h, int level, int* indptr, int* indices);
+int ge_hier_free(ge_hier* h);
+
+/* Replaces partition::interpolationMatrix(numCols, partition)
+ * (src/partitioner.cpp:29-65) in flattened form: sets[offsets[r]..offsets[r+1])
+ * are row r's columns. */
+int ge_interpolation_matrix(int num_cols, int num_rows, const int* offsets,
+                            const int* sets, ge_csr** out);
+
+/* ---- P^T A P on the device ----
+ * Replaces P_T.Mult(A).Mult(P_T.Transpose()) (examples/embed.cpp:96-98,
+ * examples/embedder.cpp:213-216; linalgcpp).  Output rows sorted ascending. */
+int ge_ptap(ge_ctx* ctx, int n, const int* indptr, const int* indices, const double* data,
+            int m, const int* pt_indptr, const int* pt_indices, ge_csr** out);
+int ge_csr_shape(const ge_csr* c, int* rows, int* cols, long long* nnz);
+int ge_csr_copy(const ge_csr* c, int* indptr, int* indices, double* data);
+int ge_csr_free(ge_csr* c);
+
+/* ---- modularity (src/partitioner.cpp:69-114) ---- */
+int ge_modularity(int n, const int* indptr, const int* indices, const double* data,
+                  int m, const int* vertex_A, double* q);
+
+/* ---- multilevel embed ----
+ * Replaces partition::embed(As, P_Ts, d) (include/embed.hpp:70-72,
+ * src/embed.cpp:561-796).  levels = P_Ts.size(); As has levels+1 entries.
+ * a_* are the concatenated CSR arrays of As[0..levels], p_* of
+ * P_Ts[0..levels-1]; a_n[l] = rows of As[l]; *_off / *_nz_off = start of each
+ * level in the indptr / indices arrays.  base_iterations / ml_iterations:
+ * reference values 100000 and 100.  print_progress mirrors the reference's
+ * "embedding layer" stdout lines (:583, :613). */
+int ge_embed(ge_ctx* ctx, int levels, const int* a_n, const int* a_off,
+             const int* a_nz_off, const int* a_indptr, const int* a_indices,
+             const double* a_data, const int* p_rows, const int* p_off,
+             const int* p_nz_off, const int* p_indptr, const int* p_indices, int dim,
+             int base_iterations, int ml_iterations, int print_progress,
+             const ge_fa_params* p, double* coords_out);
+
+/* Radius ("kinetic ball") step between levels, src/embed.cpp:615-777 (host).
+ * m coarse vertices with coords_A (m*dim, updated in place by the rescale of
+ * :757-777 unless coarse_is_base) -> r_A (m).  coarse_is_base selects the
+ * all-pairs base case (:616-679); otherwise P_T[l+1] (mc rows), coords_Ac /
+ * r_Ac of level l+2 and A_c = As[l+1] (ac_indptr/ac_indices) are used. */
+int ge_radius_step(int m, double* coords_A, double* r_A, int dim, int coarse_is_base, int mc,
+                   const int* ptc_indptr, const int* ptc_indices, const double* coords_Ac,
+                   const double* r_Ac, const int* ac_indptr, const int* ac_indices);
+
+/* The reference's initial-coordinate stream: the first `count` values of
+ * uniform_real_distribution<double>(-1,1) over mt19937(seed) (libstdc++). */
+int ge_uniform_stream(unsigned seed, long long count, double* out);
+
+/* ---- synthetic inputs (bench / tests) ----
+ * Graph500 R-MAT (0.57, 0.19, 0.19, 0.05) with a counter-based SplitMix64
+ * generator (definition: tests/graphs.py), symmetrised, deduplicated, unit
+ * weights; and the largest connected component as examples/embedder.cpp:35-93. */
+int ge_rmat_csr(int n, long long draws, unsigned long long seed, ge_csr** out);
+int ge_largest_component(int n, const int* indptr, const int* indices, const double* data,
+                         ge_csr** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GE_H */

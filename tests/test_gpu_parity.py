@@ -1,0 +1,220 @@
+"""GPU parity: the HIP path through the C ABI against the oracle and the golden
+fixtures.  STRICT mode must be bit-identical (fp64 == fp64, same bits); FAST
+mode must stay within the north star's 1e-5 relative bar.
+"""
+import numpy as np
+import pytest
+
+import ge_amd as ge
+import graphs as G
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL_FAST = 1e-5  # north star: coordinates within 1e-5 relative
+
+
+def rel_err(x, ref):
+    return float(np.max(np.abs(x - ref)) / np.max(np.abs(ref)))
+
+
+# --------------------------------------------------------------------------
+# single-level forceAtlas
+
+def test_fa_golden_supplied_init(ctx, golden):
+    g = golden("fa_er300_d3")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    for it in (1, 10, 100):
+        X = ctx.force_atlas(A, 3, coords=g["x0"], iterations=it)
+        assert np.array_equal(X, g[f"x_it{it}"]), it
+
+
+def test_fa_golden_random_init(ctx, golden):
+    g = golden("fa_rmat_d2_seeded")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    X = ctx.force_atlas(A, 2, iterations=20, seed=int(g["seed"]))
+    assert np.array_equal(X, g["x_it20"])
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3, 4])
+def test_fa_small_kernel_dims(ctx, oracle, dim):
+    A = G.erdos_renyi(97, 0.06, seed=dim)
+    X0 = G.random_coords(97, dim, seed=dim)
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=30)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=30), want)
+
+
+@pytest.mark.parametrize("n,dim", [(1025, 3), (3000, 3), (2500, 2), (1300, 4)])
+def test_fa_tiled_kernel_bitexact(ctx, oracle, n, dim):
+    A = G.largest_component(G.rmat(n + n // 3, 8 * n, seed=n))
+    m = len(A[0]) - 1
+    assert m > 1024  # the multi-block (plan) path, not the one-workgroup path
+    X0 = G.random_coords(m, dim, seed=1)
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=5)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=5), want)
+
+
+def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
+    # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
+    # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
+    A = G.largest_component(G.rmat(40, 120, seed=3))
+    want = oracle.force_atlas(A, 3, iterations=100000, seed=555)
+    got = ctx.force_atlas(A, 3, iterations=100000, seed=555)
+    assert np.array_equal(got, want)
+
+
+def test_fa_nondefault_params(ctx, oracle):
+    A = G.erdos_renyi(1500, 0.004, seed=5)
+    X0 = G.random_coords(1500, 3, seed=2)
+    kw = dict(ks=0.2, ksmax=2.0, repel=1.5, attract=0.7, gravity=2.0, use_weights=0, tolerate=0.5)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=4, **kw)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=4, **kw), want)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=3, normalize=1)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3, normalize=1), want)
+
+
+def test_fa_edge_cases(ctx, oracle):
+    one = (np.array([0, 0], np.int32), np.zeros(0, np.int32), np.zeros(0))
+    X = ctx.force_atlas(one, 3, coords=np.array([[0.5, -0.25, 0.125]]), iterations=7)
+    assert np.array_equal(X, oracle.force_atlas(one, 3, coords=np.array([[0.5, -0.25, 0.125]]),
+                                                iterations=7))
+    # isolated vertices + coincident points (distance clamped to eps)
+    A = G.erdos_renyi(30, 0.05, seed=9)
+    X0 = G.random_coords(30, 2, seed=3)
+    X0[5] = X0[6]
+    want = oracle.force_atlas(A, 2, coords=X0, iterations=10)
+    assert np.array_equal(ctx.force_atlas(A, 2, coords=X0, iterations=10), want, equal_nan=True)
+    assert ctx.force_atlas(one, 2, coords=np.zeros((1, 2)), iterations=0).shape == (1, 2)
+
+
+def test_fa_fast_mode_tolerance(ctx, oracle):
+    A = G.largest_component(G.rmat(3000, 24000, seed=11))
+    m = len(A[0]) - 1
+    X0 = G.random_coords(m, 3, seed=4)
+    strict = ctx.force_atlas(A, 3, coords=X0, iterations=30)
+    fast = ctx.force_atlas(A, 3, coords=X0, iterations=30, mode=ge.MODE_FAST)
+    assert rel_err(fast, strict) < REL_TOL_FAST
+
+
+def test_fa_plan_row_shards_compose(ctx, oracle):
+    """Two row shards stepping over a shared coordinate array (what each rank of
+    the multi-GPU path runs between all-gathers) equal the unsharded iteration."""
+    torch = pytest.importorskip("torch")
+    A = G.largest_component(G.rmat(2600, 20000, seed=21))
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=8)
+    dev = torch.device("cuda:0")
+    ip = torch.from_numpy(A[0].astype(np.int32)).to(dev)
+    ix = torch.from_numpy(A[1].astype(np.int32)).to(dev)
+    dx = torch.from_numpy(A[2]).to(dev)
+    x = torch.from_numpy(X0.copy()).to(dev)
+    y = torch.empty_like(x)
+    half = n // 2
+    plans = [ctx.fa_plan(n, len(A[1]), ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), 3, lo, hi)
+             for lo, hi in ((0, half), (half, n))]
+    for _ in range(6):
+        for p in plans:
+            p.step(x.data_ptr(), y.data_ptr())
+        x, y = y, x
+    ctx.sync()
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=6)
+    assert np.array_equal(x.cpu().numpy(), want)
+
+
+# --------------------------------------------------------------------------
+# multilevel
+
+def test_faml_golden(ctx, golden):
+    g = golden("faml_rmat4096_l0")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    X = ctx.force_atlas_ml(A, (g["P_ip"], g["P_ix"]), g["vA"], g["cA"], g["rA"], 3,
+                           iterations=100, seed=int(g["seed"]))
+    assert np.array_equal(X, g["x_it100"])
+
+
+def _block_partition(n, sizes, seed=0):
+    """P_T with aggregates of the given sizes over a random permutation of 0..n-1,
+    members listed ascending (as the partitioner emits them)."""
+    assert sum(sizes) == n
+    perm = np.random.RandomState(seed).permutation(n)
+    ip = np.cumsum([0] + list(sizes)).astype(np.int32)
+    ix = np.concatenate([np.sort(perm[ip[a]:ip[a + 1]]) for a in range(len(sizes))])
+    return ip, ix.astype(np.int32)
+
+
+@pytest.mark.parametrize("sizes", [
+    [1, 2, 3, 5, 8, 13, 21, 34, 64, 9],            # packed 64-lane blocks
+    [65, 100, 256, 3, 200],                         # 256-member packs
+    [257, 1000, 4096, 17],                          # one aggregate per block, LDS-resident
+    [5000, 300, 40, 1],                             # streamed (> 4096) path
+])
+def test_faml_size_classes(ctx, oracle, sizes):
+    n = sum(sizes)
+    A = G.submatrix(G.rmat(n, 6 * n, seed=len(sizes)), np.arange(n))
+    PT = _block_partition(n, sizes, seed=n)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, 3, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    it = 4 if n > 4000 else 12
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=it, seed=31)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=it, seed=31)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("dim", [2, 4])
+def test_faml_dims(ctx, oracle, dim):
+    A = G.largest_component(G.rmat(1500, 9000, seed=dim))
+    PT = oracle.partition(A, 0.125)[0]
+    vA = ge.vertex_of(PT)
+    cA = G.random_coords(PT[2], dim, seed=1)
+    rA = np.random.RandomState(2).uniform(0.1, 0.4, PT[2])
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=20, seed=5)
+    assert np.array_equal(ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=20, seed=5),
+                          want)
+
+
+# --------------------------------------------------------------------------
+# P^T A P and end-to-end embed
+
+def test_ptap_golden(ctx, golden):
+    g = golden("partition_rmat4096")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    for l in range(int(g["levels"])):
+        PT = (g[f"P{l}_ip"], g[f"P{l}_ix"])
+        C = ctx.ptap(A, PT)
+        want = (g[f"A{l + 1}_ip"], g[f"A{l + 1}_ix"], g[f"A{l + 1}_dx"])
+        for a, b in zip(C, want):
+            assert np.array_equal(a, b)
+        A = C
+
+
+def test_ptap_nonunit_weights(ctx, oracle):
+    A = G.largest_component(G.rmat(3000, 20000, seed=4))
+    A = (A[0], A[1], np.random.RandomState(1).uniform(0.1, 2.0, len(A[1])))
+    PT = oracle.partition(A, 0.2)[0]
+    C = ctx.ptap(A, PT)
+    for a, b in zip(C, oracle.ptap(A, PT)):
+        assert np.array_equal(a, b)
+
+
+def test_embed_c1_golden(ctx, golden):
+    g = golden("embed_c1_er1000_d2")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    hier = ge.partition(A, 0.1)
+    As = [A]
+    for PT in hier:
+        As.append(ctx.ptap(As[-1], PT))
+    X = ctx.embed(As, hier, 2, seed=int(g["seed"]))
+    assert np.array_equal(X, g["coords"])
+
+
+def test_embed_rmat_vs_oracle(ctx, oracle):
+    A = G.largest_component(G.rmat(6000, 50000, seed=12345))
+    hier = ge.partition(A, 0.125)[:4]  # examples/embedder.cpp:189-192 truncation pattern
+    As = [A]
+    for PT in hier:
+        As.append(ctx.ptap(As[-1], PT))
+    X = ctx.embed(As, hier, 3, seed=9, base_iterations=20000)
+    want = oracle.embed(As, hier, 3, seed=9, base_iterations=20000)
+    assert np.array_equal(X, want)
+    assert np.isfinite(X).all()
