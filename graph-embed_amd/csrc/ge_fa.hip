@@ -37,53 +37,13 @@
 #include <vector>
 
 #include "ge_internal.hpp"
+#include "ge_pair.hpp"
 
 namespace ge {
 namespace {
 
-constexpr double kEps = 0.00001;  // include/forceatlas.hpp:110
-
-struct FaConst {
-  double ks_gS;    // ks * globalSpeed (globalSpeed = tolerate * 1.0 / 1.0)
-  double gS;       // globalSpeed
-  double ksmax, repel, attract, gravity, delta;
-  int use_weights, linlog, nohubs;
-};
-
-FaConst make_const(const ge_fa_params& p) {
-  FaConst c;
-  c.gS = p.tolerate * 1.0 / 1.0;  // :244 with :228, :242
-  c.ks_gS = p.ks * c.gS;
-  c.ksmax = p.ksmax;
-  c.repel = p.repel;
-  c.attract = p.attract;
-  c.gravity = p.gravity;
-  c.delta = p.delta;
-  c.use_weights = p.use_weights;
-  c.linlog = p.linlog;
-  c.nohubs = p.nohubs;
-  return c;
-}
-
-__device__ __forceinline__ double clamp_eps(double x) { return x < kEps ? kEps : x; }
-
-// Attraction magnitude, include/forceatlas.hpp:176-196.  The linlog / delta != 1
-// branches call device log/pow (ocml), which may differ from glibc in the last
-// ulp: only the default branch is bit-exact.
-__device__ __forceinline__ double attraction_mag(double dis, double a, double dip1,
-                                                 const FaConst& c) {
-  double f = dis;
-  if (c.linlog) f = log(1 + f);
-  if (c.delta == 1.0) {
-    f = f * a;
-  } else if (c.delta != 0.0) {
-    double sgn = (a < 0) ? -1.0 : 1.0;
-    double mg = (a < 0) ? -a : a;
-    f = sgn * pow(mg, c.delta) * f;
-  }
-  if (c.nohubs) f = f / dip1;
-  return c.attract * f;
-}
+constexpr double kEps = kFaEps;
+FaConst make_const(const ge_fa_params& p) { return make_fa_const(p); }
 
 // deg[i] + 1 with deg the serial row sum of include/forceatlas.hpp:127-140.
 __global__ void degp1_kernel(int n, const int* __restrict__ ip, const double* __restrict__ dx,
@@ -122,6 +82,7 @@ fa_repulse_strict(int n, int rb, int re, const double* __restrict__ X,
   const int base = rb + blockIdx.x * (kRepThreads * R);
 
   double xi[R][D], di[R], acc[R][D];
+  bool rows_ok = true;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int i = base + tid + r * kRepThreads;
@@ -132,37 +93,40 @@ fa_repulse_strict(int n, int rb, int re, const double* __restrict__ X,
       acc[r][k] = 0.0;
     }
     di[r] = ok ? dp1[i] : 1.0;
+    rows_ok = rows_ok && vertex_ok<D>(xi[r], di[r]);
   }
+  if (!REPEL_ONE) rows_ok = rows_ok && weight_ok(repel);
 
   for (int j0 = 0; j0 < n; j0 += kTileJ) {
     const int cnt = min(kTileJ, n - j0);
     __syncthreads();
+    bool ok = rows_ok;
     if (tid < cnt) {
       const int j = j0 + tid;
 #pragma unroll
-      for (int k = 0; k < D; ++k) tile[tid * W + k] = X[(size_t)j * D + k];
+      for (int k = 0; k < D; ++k) {
+        const double v = X[(size_t)j * D + k];
+        tile[tid * W + k] = v;
+        ok = ok && coord_ok(v);
+      }
       tile[tid * W + D] = dp1[j];
+      ok = ok && weight_ok(dp1[j]);
     }
-    __syncthreads();
-    for (int jj = 0; jj < cnt; ++jj) {
-      double xj[D];
+    // block-uniform: every coordinate of this tile and every row of the block
+    // is in the exact shared-reciprocal domain (ge_math.hpp)
+    if (__syncthreads_and(ok)) {
+      for (int jj = 0; jj < cnt; ++jj) {
+        const double* xj = &tile[jj * W];
+        const double dj = tile[jj * W + D];
 #pragma unroll
-      for (int k = 0; k < D; ++k) xj[k] = tile[jj * W + k];
-      const double dj = tile[jj * W + D];
+        for (int r = 0; r < R; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+      }
+    } else {
+      for (int jj = 0; jj < cnt; ++jj) {
+        const double* xj = &tile[jj * W];
+        const double dj = tile[jj * W + D];
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        double e[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) e[k] = xi[r][k] - xj[k];
-        double s = e[0] * e[0];
-#pragma unroll
-        for (int k = 1; k < D; ++k) s = s + e[k] * e[k];
-        const double dis = clamp_eps(sqrt(s));
-        double cij = di[r] * dj;
-        if (!REPEL_ONE) cij = cij * repel;
-        const double val = cij / (dis * dis);
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + (e[k] / dis) * val;
+        for (int r = 0; r < R; ++r) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
       }
     }
   }
@@ -282,11 +246,11 @@ __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D],
 #pragma unroll
   for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
   const double mag = sqrt(m2);  // not clamped (:205)
-  double F[D];
+  double unit[D], F[D];
+  neg_over<D>(xi, mag, unit);
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    const double unit = -xi[k] / mag;
-    const double g = unit * c.gravity * dip1;
+    const double g = unit[k] * c.gravity * dip1;
     F[k] = acc[k] + g;
   }
   double s = 0.0, f2 = 0.0;
@@ -323,21 +287,16 @@ fa_attract_update_strict(int rb, int re, const int* __restrict__ ip, const int* 
     xi[k] = X[(size_t)i * D + k];
     acc[k] = Frep[(size_t)li * D + k];
   }
+  const bool row_ok = all_coord_ok<D>(xi);
   const double dip1 = dp1[i];
   const int e1 = ip[i + 1];
   for (int e = ip[i]; e < e1; ++e) {
-    const int j = ix[e];
-    double t[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) t[k] = X[(size_t)j * D + k] - xi[k];
-    double s = t[0] * t[0];
-#pragma unroll
-    for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
-    const double dis = clamp_eps(sqrt(s));
+    const double* xj = X + (size_t)ix[e] * D;
     const double a = c.use_weights ? dx[e] : 1.0;
-    const double Fa = attraction_mag(dis, a, dip1, c);
-#pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+    if (row_ok && all_coord_ok<D>(xj))
+      attr_edge<D, true>(xi, xj, a, dip1, c, acc);
+    else
+      attr_edge<D, false>(xi, xj, a, dip1, c, acc);
   }
   finish_row<D>(i, li, xi, acc, dip1, c, Fprev, Xnext);
 }
@@ -380,43 +339,31 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
         acc[k] = 0.0;
       }
       const double dip1 = sx[i * W + D];
+      const bool row_ok = all_coord_ok<D>(xi);
+      const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
       for (int j = 0; j < n; ++j) {
-        double e[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) e[k] = xi[k] - sx[j * W + k];
-        double s = e[0] * e[0];
-#pragma unroll
-        for (int k = 1; k < D; ++k) s = s + e[k] * e[k];
-        const double dis = clamp_eps(sqrt(s));
-        double cij = dip1 * sx[j * W + D];
-        cij = cij * c.repel;
-        const double val = cij / (dis * dis);
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+        const double* xj = &sx[j * W];
+        if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
+          rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, acc);
+        else
+          rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, acc);
       }
       for (int e = ip[i]; e < ip[i + 1]; ++e) {
-        const int j = ix[e];
-        double t[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = sx[j * W + k] - xi[k];
-        double s = t[0] * t[0];
-#pragma unroll
-        for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
-        const double dis = clamp_eps(sqrt(s));
+        const double* xj = &sx[ix[e] * W];
         const double a = c.use_weights ? dx[e] : 1.0;
-        const double Fa = attraction_mag(dis, a, dip1, c);
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+        if (row_ok && all_coord_ok<D>(xj))
+          attr_edge<D, true>(xi, xj, a, dip1, c, acc);
+        else
+          attr_edge<D, false>(xi, xj, a, dip1, c, acc);
       }
       double m2 = xi[0] * xi[0];
 #pragma unroll
       for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
       const double mag = sqrt(m2);
+      double unit[D];
+      neg_over<D>(xi, mag, unit);
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        const double unit = -xi[k] / mag;
-        F[r][k] = acc[k] + unit * c.gravity * dip1;
-      }
+      for (int k = 0; k < D; ++k) F[r][k] = acc[k] + unit[k] * c.gravity * dip1;
     }
     __syncthreads();
 #pragma unroll
@@ -488,17 +435,6 @@ void launch_attract(hipStream_t s, int rb, int re, const int* ip, const int* ix,
   if (rows <= 0) return;
   hipLaunchKernelGGL((fa_attract_update_strict<D>), dim3((rows + 255) / 256), dim3(256), 0, s,
                      rb, re, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c);
-}
-
-template <class F>
-void dispatch_dim(int dim, F&& f) {
-  switch (dim) {
-    case 1: f(std::integral_constant<int, 1>()); break;
-    case 2: f(std::integral_constant<int, 2>()); break;
-    case 3: f(std::integral_constant<int, 3>()); break;
-    case 4: f(std::integral_constant<int, 4>()); break;
-    default: throw Error(GE_ERR_ARG, "dimension must be 1..4");
-  }
 }
 
 }  // namespace

@@ -33,33 +33,13 @@
 #include <vector>
 
 #include "ge_internal.hpp"
+#include "ge_pair.hpp"
 
 namespace ge {
 namespace {
 
-constexpr double kEps = 0.00001;
-
-struct MlConst {
-  double ks_gS, gS, ksmax, repel, attract, gravity, delta;
-  int use_weights, linlog, nohubs;
-};
-
-__device__ __forceinline__ double clamp_eps(double x) { return x < kEps ? kEps : x; }
-
-__device__ __forceinline__ double attraction_mag(double dis, double a, double dip1,
-                                                 const MlConst& c) {
-  double f = dis;
-  if (c.linlog) f = log(1 + f);
-  if (c.delta == 1.0) {
-    f = f * a;
-  } else if (c.delta != 0.0) {
-    double sgn = (a < 0) ? -1.0 : 1.0;
-    double mg = (a < 0) ? -a : a;
-    f = sgn * pow(mg, c.delta) * f;
-  }
-  if (c.nohubs) f = f / dip1;
-  return c.attract * f;
-}
+constexpr double kEps = kFaEps;
+using MlConst = FaConst;
 
 template <int D>
 struct W {
@@ -80,6 +60,28 @@ __device__ __forceinline__ double internal_dp1(int v, int a, const int* __restri
   return s + 1;
 }
 
+// ((t / dis) * 100.0) / mag for the external pull of one CSR entry (:452-465).
+template <int D, bool SHARED>
+__device__ __forceinline__ void pull_edge(const double* __restrict__ ca,
+                                          const double* __restrict__ cb, double mag,
+                                          const Recip& rmag, double (&acc)[D]) {
+  double t[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) t[k] = cb[k] - ca[k];
+  double q = t[0] * t[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k) q = q + t[k] * t[k];
+  const double dis = clamp_eps(sqrt(q));
+  if (SHARED) {
+    const Recip rc = recip_of(dis);
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by(div_by(t[k], dis, rc) * 100.0, mag, rmag);
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * 100.0 / mag;
+  }
+}
+
 // Force on one member (:391-474).  xs(l) returns the coordinates of local member
 // l of the same aggregate; xi/dip1 the member's own.
 template <int D, class XS, class DS>
@@ -94,59 +96,45 @@ __device__ __forceinline__ void member_force(int li, int s, int a, int v, const 
   double acc[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) acc[k] = 0.0;
-  for (int j = 0; j < s; ++j) {
-    double e[D];
+  const bool row_ok = all_coord_ok<D>(xi);
+  const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
+  for (int j = 0; j < s; ++j) {  // :394-410
     const double* xj = xs(j);
-#pragma unroll
-    for (int k = 0; k < D; ++k) e[k] = xi[k] - xj[k];
-    double q = e[0] * e[0];
-#pragma unroll
-    for (int k = 1; k < D; ++k) q = q + e[k] * e[k];
-    const double dis = clamp_eps(sqrt(q));
-    const double val = dip1 * ds(j) * c.repel / (dis * dis);
-#pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+    if (rep_ok && vertex_ok<D>(xj, ds(j)))
+      rep_pair<D, true, false>(xi, xj, dip1, ds(j), c.repel, acc);
+    else
+      rep_pair<D, false, false>(xi, xj, dip1, ds(j), c.repel, acc);
   }
   double m2 = xi[0] * xi[0];
 #pragma unroll
   for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
   double mag = sqrt(m2);
   if (mag < kEps) mag = kEps;
+  const Recip rmag = recip_of(mag);
   const double* ca = cA + (size_t)a * D;
-  for (int e = ip[v]; e < ip[v + 1]; ++e) {
+  const bool ca_ok = all_coord_ok<D>(ca);
+  for (int e = ip[v]; e < ip[v + 1]; ++e) {  // :415-467
     const int j = ix[e];
     const int b = vA[j];
-    if (b == a && j != li) {
+    if (b == a && j != li) {  // sic: global j against local i (:417)
       const double* xj = xs(pos_of[j] - pt_base);
-      double t[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) t[k] = xj[k] - xi[k];
-      double q = t[0] * t[0];
-#pragma unroll
-      for (int k = 1; k < D; ++k) q = q + t[k] * t[k];
-      const double dis = clamp_eps(sqrt(q));
       const double w = c.use_weights ? dx[e] : 1.0;
-      const double Fa = attraction_mag(dis, w, dip1, c);
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+      if (row_ok && all_coord_ok<D>(xj))
+        attr_edge<D, true>(xi, xj, w, dip1, c, acc);
+      else
+        attr_edge<D, false>(xi, xj, w, dip1, c, acc);
     } else {
       const double* cb = cA + (size_t)b * D;
-      double t[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) t[k] = cb[k] - ca[k];
-      double q = t[0] * t[0];
-#pragma unroll
-      for (int k = 1; k < D; ++k) q = q + t[k] * t[k];
-      const double dis = clamp_eps(sqrt(q));
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * 100.0 / mag;
+      if (row_ok && ca_ok && all_coord_ok<D>(cb))
+        pull_edge<D, true>(ca, cb, mag, rmag, acc);
+      else
+        pull_edge<D, false>(ca, cb, mag, rmag, acc);
     }
   }
+  double unit[D];
+  neg_over<D>(xi, mag, unit);
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    const double unit = -xi[k] / mag;
-    F[k] = acc[k] + unit * c.gravity * dip1;
-  }
+  for (int k = 0; k < D; ++k) F[k] = acc[k] + unit[k] * c.gravity * dip1;  // :469-474
 }
 
 // Swing (clamped) + speed + update of one member (:477-530).
@@ -361,6 +349,8 @@ faml_huge_force(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
     acc[k] = 0.0;
   }
   const double dip1 = DP[cpos];
+  const bool row_ok = all_coord_ok<D>(xi);
+  const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
   for (int j0 = 0; j0 < s; j0 += kHT) {
     const int cnt = min(kHT, s - j0);
     __syncthreads();
@@ -372,16 +362,11 @@ faml_huge_force(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
     }
     __syncthreads();
     for (int jj = 0; jj < cnt; ++jj) {
-      double e[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) e[k] = xi[k] - tile[jj * WV + k];
-      double q = e[0] * e[0];
-#pragma unroll
-      for (int k = 1; k < D; ++k) q = q + e[k] * e[k];
-      const double dis = clamp_eps(sqrt(q));
-      const double val = dip1 * tile[jj * WV + D] * c.repel / (dis * dis);
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+      const double* xj = &tile[jj * WV];
+      if (rep_ok && vertex_ok<D>(xj, tile[jj * WV + D]))
+        rep_pair<D, true, false>(xi, xj, dip1, tile[jj * WV + D], c.repel, acc);
+      else
+        rep_pair<D, false, false>(xi, xj, dip1, tile[jj * WV + D], c.repel, acc);
     }
   }
   if (!ok) return;
@@ -391,42 +376,32 @@ faml_huge_force(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
   for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
   double mag = sqrt(m2);
   if (mag < kEps) mag = kEps;
+  const Recip rmag = recip_of(mag);
   const double* ca = cA + (size_t)a * D;
+  const bool ca_ok = all_coord_ok<D>(ca);
   const int v = pt_ix[cpos];
   for (int e = ip[v]; e < ip[v + 1]; ++e) {
     const int j = ix[e];
     const int b = vA[j];
     if (b == a && j != li) {
       const double* xj = Xp + (size_t)pos_of[j] * D;
-      double t[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) t[k] = xj[k] - xi[k];
-      double q = t[0] * t[0];
-#pragma unroll
-      for (int k = 1; k < D; ++k) q = q + t[k] * t[k];
-      const double dis = clamp_eps(sqrt(q));
       const double w = c.use_weights ? dx[e] : 1.0;
-      const double Fa = attraction_mag(dis, w, dip1, c);
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+      if (row_ok && all_coord_ok<D>(xj))
+        attr_edge<D, true>(xi, xj, w, dip1, c, acc);
+      else
+        attr_edge<D, false>(xi, xj, w, dip1, c, acc);
     } else {
       const double* cb = cA + (size_t)b * D;
-      double t[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) t[k] = cb[k] - ca[k];
-      double q = t[0] * t[0];
-#pragma unroll
-      for (int k = 1; k < D; ++k) q = q + t[k] * t[k];
-      const double dis = clamp_eps(sqrt(q));
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * 100.0 / mag;
+      if (row_ok && ca_ok && all_coord_ok<D>(cb))
+        pull_edge<D, true>(ca, cb, mag, rmag, acc);
+      else
+        pull_edge<D, false>(ca, cb, mag, rmag, acc);
     }
   }
+  double unit[D];
+  neg_over<D>(xi, mag, unit);
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    const double unit = -xi[k] / mag;
-    Fscr[(size_t)cpos * D + k] = acc[k] + unit * c.gravity * dip1;
-  }
+  for (int k = 0; k < D; ++k) Fscr[(size_t)cpos * D + k] = acc[k] + unit[k] * c.gravity * dip1;
 }
 
 template <int D>
@@ -511,17 +486,6 @@ __global__ void pos_of_kernel(int N, const int* __restrict__ pt_ix, int* __restr
   if (c < N) pos_of[pt_ix[c]] = c;
 }
 
-template <class F>
-void dispatch_dim(int dim, F&& f) {
-  switch (dim) {
-    case 1: f(std::integral_constant<int, 1>()); break;
-    case 2: f(std::integral_constant<int, 2>()); break;
-    case 3: f(std::integral_constant<int, 3>()); break;
-    case 4: f(std::integral_constant<int, 4>()); break;
-    default: throw Error(GE_ERR_ARG, "dimension must be 1..4");
-  }
-}
-
 // Greedy packs over `ids` (already size-sorted) with total members <= cap.
 void build_packs(const std::vector<int>& ids, const int* h_pt_ip, int cap, int max_aggs,
                  std::vector<int>& order, std::vector<int>& beg) {
@@ -551,17 +515,7 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
   hipStream_t st = ctx->stream;
   const int N = h_pt_ip[m];
   GE_REQUIRE(N == n, "P_T must have one entry per fine vertex");
-  MlConst c;
-  c.gS = p.tolerate * 1.0 / 1.0;
-  c.ks_gS = p.ks * c.gS;
-  c.ksmax = p.ksmax;
-  c.repel = p.repel;
-  c.attract = p.attract;
-  c.gravity = p.gravity;
-  c.delta = p.delta;
-  c.use_weights = p.use_weights;
-  c.linlog = p.linlog;
-  c.nohubs = p.nohubs;
+  const MlConst c = make_fa_const(p);
 
   // bucket aggregates by size (largest first inside each bucket)
   std::vector<int> small, mid, large, huge;

@@ -1,0 +1,157 @@
+// ge_pair.hpp -- per-pair / per-edge ForceAtlas terms shared by the kernels.
+//
+// Each function evaluates one term of include/forceatlas.hpp exactly as the
+// reference writes it (operand order, one rounding per operation).  With
+// SHARED = true the three divisions by one denominator reuse its reciprocal
+// (ge_math.hpp): same instructions, same bits, valid when the caller has checked
+// coord_ok() for every coordinate involved.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ge_internal.hpp"
+#include "ge_math.hpp"
+
+namespace ge {
+
+constexpr double kFaEps = 0.00001;  // include/forceatlas.hpp:110, :337
+
+struct FaConst {
+  double ks_gS;  // ks * globalSpeed, globalSpeed = tolerate * 1.0 / 1.0 (:228, :242, :244)
+  double gS;
+  double ksmax, repel, attract, gravity, delta;
+  int use_weights, linlog, nohubs;
+};
+
+inline FaConst make_fa_const(const ge_fa_params& p) {
+  FaConst c;
+  c.gS = p.tolerate * 1.0 / 1.0;
+  c.ks_gS = p.ks * c.gS;
+  c.ksmax = p.ksmax;
+  c.repel = p.repel;
+  c.attract = p.attract;
+  c.gravity = p.gravity;
+  c.delta = p.delta;
+  c.use_weights = p.use_weights;
+  c.linlog = p.linlog;
+  c.nohubs = p.nohubs;
+  return c;
+}
+
+__device__ __forceinline__ double clamp_eps(double x) { return x < kFaEps ? kFaEps : x; }
+
+// Attraction magnitude (:176-196).  linlog / delta != 1 use device log / pow
+// (ocml), which may differ from glibc in the last ulp: only the default branch
+// is bit-exact.
+__device__ __forceinline__ double attraction_mag(double dis, double a, double dip1,
+                                                 const FaConst& c) {
+  double f = dis;
+  if (c.linlog) f = log(1 + f);
+  if (c.delta == 1.0) {
+    f = f * a;
+  } else if (c.delta != 0.0) {
+    const double sgn = (a < 0) ? -1.0 : 1.0;
+    const double mg = (a < 0) ? -a : a;
+    f = sgn * pow(mg, c.delta) * f;
+  }
+  if (c.nohubs) f = f / dip1;
+  return c.attract * f;
+}
+
+// Repulsion of j on i (:152-166), accumulated into acc.  e = x_i - x_j equals
+// -(x_j - x_i) up to the sign of zero, and a zero term never changes the sum
+// (see ge_fa.hip); the j == i term is +0 for the same reason.
+template <int D, bool SHARED, bool REPEL_ONE>
+__device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __restrict__ xj,
+                                         double dip1, double djp1, double repel,
+                                         double (&acc)[D]) {
+  double e[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) e[k] = xi[k] - xj[k];
+  double s = e[0] * e[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k) s = s + e[k] * e[k];
+  double cij = dip1 * djp1;
+  if (!REPEL_ONE) cij = cij * repel;
+  if (SHARED) {
+    // in-domain: s == 0 or s >= 2^-504, deg+1 and repel in [2^-60, 2^60]
+    const double dis = clamp_eps(s == 0.0 ? 0.0 : sqrt_normal(s));
+    const double dd = dis * dis;
+    const double val = div_by(cij, dd, recip_of(dd));
+    const Recip rc = recip_of(dis);
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by(e[k], dis, rc) * val;
+  } else {
+    const double dis = clamp_eps(sqrt(s));
+    const double val = cij / (dis * dis);
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+  }
+}
+
+// Attraction along one CSR entry (:169-203): t = x_j - x_i.
+template <int D, bool SHARED>
+__device__ __forceinline__ void attr_edge(const double (&xi)[D], const double* __restrict__ xj,
+                                          double a, double dip1, const FaConst& c,
+                                          double (&acc)[D]) {
+  double t[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) t[k] = xj[k] - xi[k];
+  double s = t[0] * t[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
+  const double dis = clamp_eps(SHARED ? (s == 0.0 ? 0.0 : sqrt_normal(s)) : sqrt(s));
+  const double Fa = attraction_mag(dis, a, dip1, c);
+  if (SHARED) {
+    const Recip rc = recip_of(dis);
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by(t[k], dis, rc) * Fa;
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (t[k] / dis) * Fa;
+  }
+}
+
+template <int D>
+__device__ __forceinline__ bool all_coord_ok(const double* x) {
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < D; ++k) ok = ok && coord_ok(x[k]);
+  return ok;
+}
+
+// A vertex whose coordinates and deg+1 lie in the exact shared-reciprocal
+// domain of rep_pair<SHARED = true>.
+template <int D>
+__device__ __forceinline__ bool vertex_ok(const double* x, double dp1) {
+  return all_coord_ok<D>(x) && weight_ok(dp1);
+}
+
+// -x_k / mag for all k (:208 single level, :471 multilevel).
+template <int D>
+__device__ __forceinline__ void neg_over(const double (&x)[D], double mag, double (&out)[D]) {
+  double nx[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) nx[k] = -x[k];
+  if (exact_den(mag) && all_coord_ok<D>(x)) {
+    const Recip rc = recip_of(mag);
+#pragma unroll
+    for (int k = 0; k < D; ++k) out[k] = div_by(nx[k], mag, rc);
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) out[k] = nx[k] / mag;
+  }
+}
+
+template <class F>
+void dispatch_dim(int dim, F&& f) {
+  switch (dim) {
+    case 1: f(std::integral_constant<int, 1>()); break;
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    case 4: f(std::integral_constant<int, 4>()); break;
+    default: throw Error(GE_ERR_ARG, "dimension must be 1..4");
+  }
+}
+
+}  // namespace ge

@@ -90,6 +90,8 @@ _SIGS = {
     "ge_radius_step": (ctypes.c_int, [ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ge_uniform_stream": (ctypes.c_int, [ctypes.c_uint, ctypes.c_longlong, _f64p]),
+    "ge_selftest_math": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_ulonglong,
+                                        ctypes.POINTER(ctypes.c_longlong)]),
     "ge_rmat_csr": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                    ctypes.POINTER(_vp)]),
     "ge_largest_component": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p,
@@ -107,6 +109,13 @@ def build():
 def lib():
     global _lib
     if _lib is None:
+        # torch ships its own libamdhip64.so.7; two HIP runtimes in one process
+        # cannot share the device.  Load torch first (when present) so libge.so
+        # binds to the runtime already in the process.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise GeError(f"{LIB_PATH} is missing: build it with `make -C {PKG_ROOT}` "
                           "(no CPU fallback exists)")
@@ -216,6 +225,11 @@ class Context:
         _check(lib().ge_embed(self.h, len(hier), *parts, dim, base_iterations, ml_iterations,
                               int(print_progress), ctypes.byref(p), out.reshape(-1)))
         return out
+
+    def selftest_math(self, samples=1 << 24, seed=1):
+        bad = ctypes.c_longlong()
+        _check(lib().ge_selftest_math(self.h, samples, seed, ctypes.byref(bad)))
+        return bad.value
 
     def fa_plan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw):
         return FaPlan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw)

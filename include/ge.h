@@ -161,6 +161,12 @@ int ge_radius_step(int m, double* coords_A, double* r_A, int dim, int coarse_is_
  * uniform_real_distribution<double>(-1,1) over mt19937(seed) (libstdc++). */
 int ge_uniform_stream(unsigned seed, long long count, double* out);
 
+/* Diagnostics: checks on the device that the strict kernels' shared-reciprocal
+ * division (graph-embed_amd/csrc/ge_math.hpp) returns the same bits as IEEE
+ * division for `samples` random and adversarial operand triples. */
+int ge_selftest_math(ge_ctx* ctx, long long samples, unsigned long long seed,
+                     long long* mismatches);
+
 /* ---- synthetic inputs (bench / tests) ----
  * Graph500 R-MAT (0.57, 0.19, 0.19, 0.05) with a counter-based SplitMix64
  * generator (definition: tests/graphs.py), symmetrised, deduplicated, unit

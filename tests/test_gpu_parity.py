@@ -18,6 +18,14 @@ def rel_err(x, ref):
 
 
 # --------------------------------------------------------------------------
+# exact arithmetic building blocks
+
+def test_shared_reciprocal_division_is_ieee(ctx):
+    # 3 checks per sample; 2^26 samples ~ 2e8 divisions compared bitwise to `/`
+    assert ctx.selftest_math(1 << 26, seed=7) == 0
+
+
+# --------------------------------------------------------------------------
 # single-level forceAtlas
 
 def test_fa_golden_supplied_init(ctx, golden):
@@ -45,7 +53,7 @@ def test_fa_small_kernel_dims(ctx, oracle, dim):
 
 @pytest.mark.parametrize("n,dim", [(1025, 3), (3000, 3), (2500, 2), (1300, 4)])
 def test_fa_tiled_kernel_bitexact(ctx, oracle, n, dim):
-    A = G.largest_component(G.rmat(n + n // 3, 8 * n, seed=n))
+    A = G.rmat(n, 8 * n, seed=n)  # isolated vertices included (gravity only)
     m = len(A[0]) - 1
     assert m > 1024  # the multi-block (plan) path, not the one-workgroup path
     X0 = G.random_coords(m, dim, seed=1)
