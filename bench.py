@@ -130,9 +130,9 @@ def main():
     X0 = ge.uniform_stream(args.seed, n * args.dim).reshape(n, args.dim)  # ref init order
     log(rank, f"R-MAT n={n} nnz={nnz} generated in {time.perf_counter() - t0:.1f}s")
 
-    chunk = (n + world - 1) // world
-    npad = chunk * world
-    rb, re = min(n, rank * chunk), min(n, (rank + 1) * chunk)
+    from ge_amd.dist import ShardedForceAtlas
+    drv = ShardedForceAtlas(n, world, rank, None)
+    npad, rb, re = drv.padded_rows, drv.rb, drv.re
     ip = torch.from_numpy(A[0]).to(dev)
     ix = torch.from_numpy(A[1]).to(dev)
     dx = torch.from_numpy(A[2]).to(dev)
@@ -146,11 +146,8 @@ def main():
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), args.dim, rb, re,
                        mode=mode)
 
-    def step(cur, nxt):
-        plan.step(cur.data_ptr(), nxt.data_ptr())
-        if world > 1:
-            mine = nxt[rank * chunk:(rank + 1) * chunk]
-            dist.all_gather_into_tensor(nxt, mine)
+    drv.step_rows = lambda cur, nxt, rb_, re_: plan.step(cur.data_ptr(), nxt.data_ptr())
+    step = drv.step
 
     cur, nxt = xa, xb
     for _ in range(args.warmup):

@@ -61,82 +61,96 @@ __global__ void degp1_kernel(int n, const int* __restrict__ ip, const double* __
 }
 
 // ---------------------------------------------------------------------------
-// STRICT repulsion.  Block = 256 threads, each owns R rows (stride 256), the j
-// range is streamed through an LDS tile of 256 records {x_0..x_{D-1}, deg+1}.
+// STRICT repulsion.  A persistent grid of one 512-thread block per CU; block b
+// owns the contiguous rows [rb + b*per, rb + (b+1)*per) and walks them in
+// chunks of 512*R rows (thread t, slot r -> row c0 + t + 512 r).  Each wave
+// skips the slots it has no rows in (wave-uniform), so the work per SIMD is
+// balanced to one 64-row slot.  The j range is streamed through an LDS tile of
+// 256 records {x_0..x_{D-1}, deg+1}; every row's sum runs over j ascending.
 
-constexpr int kRepThreads = 256;
+constexpr int kRepThreads = 512;
 constexpr int kTileJ = 256;
+constexpr int kRepR = 8;  // row slots per thread and chunk
 
 template <int D>
 struct Rec {
   static constexpr int W = (D + 1 <= 4) ? 4 : 8;  // doubles per LDS record
 };
 
-template <int D, int R, bool REPEL_ONE>
+template <int D, bool REPEL_ONE>
 __global__ void __launch_bounds__(kRepThreads)
-fa_repulse_strict(int n, int rb, int re, const double* __restrict__ X,
+fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict__ X,
                   const double* __restrict__ dp1, double repel, double* __restrict__ Frep) {
   constexpr int W = Rec<D>::W;
+  constexpr int R = kRepR;
   __shared__ __attribute__((aligned(16))) double tile[kTileJ * W];
   const int tid = threadIdx.x;
-  const int base = rb + blockIdx.x * (kRepThreads * R);
+  const int wave = tid >> 6;
+  const int bbeg = rb + blockIdx.x * per_block;
+  const int bend = min(re, bbeg + per_block);
+  const bool repel_ok = REPEL_ONE || weight_ok(repel);
 
-  double xi[R][D], di[R], acc[R][D];
-  bool rows_ok = true;
+  for (int c0 = bbeg; c0 < bend; c0 += kRepThreads * R) {
+    // slots with at least one row in this wave: r < nr (wave-uniform)
+    const int first = c0 + wave * 64;
+    const int nr = first >= bend ? 0 : min(R, (bend - first + kRepThreads - 1) / kRepThreads);
+    double xi[R][D], di[R], acc[R][D];
+    bool rows_ok = repel_ok;
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int i = base + tid + r * kRepThreads;
-    const bool ok = i < re;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      xi[r][k] = ok ? X[(size_t)i * D + k] : 0.0;
-      acc[r][k] = 0.0;
-    }
-    di[r] = ok ? dp1[i] : 1.0;
-    rows_ok = rows_ok && vertex_ok<D>(xi[r], di[r]);
-  }
-  if (!REPEL_ONE) rows_ok = rows_ok && weight_ok(repel);
-
-  for (int j0 = 0; j0 < n; j0 += kTileJ) {
-    const int cnt = min(kTileJ, n - j0);
-    __syncthreads();
-    bool ok = rows_ok;
-    if (tid < cnt) {
-      const int j = j0 + tid;
+    for (int r = 0; r < R; ++r) {
+      const int i = c0 + tid + r * kRepThreads;
+      const bool ok = i < bend;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        const double v = X[(size_t)j * D + k];
-        tile[tid * W + k] = v;
-        ok = ok && coord_ok(v);
+        xi[r][k] = ok ? X[(size_t)i * D + k] : 0.0;
+        acc[r][k] = 0.0;
       }
-      tile[tid * W + D] = dp1[j];
-      ok = ok && weight_ok(dp1[j]);
+      di[r] = ok ? dp1[i] : 1.0;
+      rows_ok = rows_ok && vertex_ok<D>(xi[r], di[r]);
     }
-    // block-uniform: every coordinate of this tile and every row of the block
-    // is in the exact shared-reciprocal domain (ge_math.hpp)
-    if (__syncthreads_and(ok)) {
-      for (int jj = 0; jj < cnt; ++jj) {
-        const double* xj = &tile[jj * W];
-        const double dj = tile[jj * W + D];
+    for (int j0 = 0; j0 < n; j0 += kTileJ) {
+      const int cnt = min(kTileJ, n - j0);
+      __syncthreads();
+      bool ok = rows_ok;
+      if (tid < cnt) {
+        const int j = j0 + tid;
 #pragma unroll
-        for (int r = 0; r < R; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+        for (int k = 0; k < D; ++k) {
+          const double v = X[(size_t)j * D + k];
+          tile[tid * W + k] = v;
+          ok = ok && coord_ok(v);
+        }
+        const double w = dp1[j];
+        tile[tid * W + D] = w;
+        ok = ok && weight_ok(w);
       }
-    } else {
-      for (int jj = 0; jj < cnt; ++jj) {
-        const double* xj = &tile[jj * W];
-        const double dj = tile[jj * W + D];
+      // block-uniform: every coordinate of this tile and of the block's rows is
+      // in the exact shared-reciprocal domain (ge_math.hpp)
+      if (__syncthreads_and(ok)) {
+        for (int jj = 0; jj < cnt; ++jj) {
+          const double* xj = &tile[jj * W];
+          const double dj = tile[jj * W + D];
 #pragma unroll
-        for (int r = 0; r < R; ++r) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+          for (int r = 0; r < R; ++r)
+            if (r < nr) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+        }
+      } else {
+        for (int jj = 0; jj < cnt; ++jj) {
+          const double* xj = &tile[jj * W];
+          const double dj = tile[jj * W + D];
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (r < nr) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+        }
       }
     }
-  }
-
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int i = base + tid + r * kRepThreads;
-    if (i < re) {
+    for (int r = 0; r < R; ++r) {
+      const int i = c0 + tid + r * kRepThreads;
+      if (i < bend) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) Frep[(size_t)(i - rb) * D + k] = acc[r][k];
+        for (int k = 0; k < D; ++k) Frep[(size_t)(i - rb) * D + k] = acc[r][k];
+      }
     }
   }
 }
@@ -149,8 +163,10 @@ fa_repulse_strict(int n, int rb, int re, const double* __restrict__ X,
 
 constexpr int kFastJBlocks = 16;  // j-range split
 
+constexpr int kFastThreads = 256;
+
 template <int D, int R>
-__global__ void __launch_bounds__(kRepThreads)
+__global__ void __launch_bounds__(kFastThreads)
 fa_repulse_fast(int n, int rb, int re, const double* __restrict__ X,
                 const double* __restrict__ dp1, double repel, int jblocks,
                 double* __restrict__ Fpart) {
@@ -158,7 +174,7 @@ fa_repulse_fast(int n, int rb, int re, const double* __restrict__ X,
   __shared__ __attribute__((aligned(16))) double tile[kTileJ * W];
   const int tid = threadIdx.x;
   const int rows_here = re - rb;
-  const int base = rb + blockIdx.x * (kRepThreads * R);
+  const int base = rb + blockIdx.x * (kFastThreads * R);
   const int jb = blockIdx.y;
   const int jchunk = (n + jblocks - 1) / jblocks;
   const int jbeg = jb * jchunk;
@@ -168,7 +184,7 @@ fa_repulse_fast(int n, int rb, int re, const double* __restrict__ X,
   double xi[R][D], di[R], acc[R][D];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int i = base + tid + r * kRepThreads;
+    const int i = base + tid + r * kFastThreads;
     const bool ok = i < re;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -215,7 +231,7 @@ fa_repulse_fast(int n, int rb, int re, const double* __restrict__ X,
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int i = base + tid + r * kRepThreads;
+    const int i = base + tid + r * kFastThreads;
     if (i < re) {
 #pragma unroll
       for (int k = 0; k < D; ++k)
@@ -398,33 +414,42 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
 // ---------------------------------------------------------------------------
 // host-side launch helpers
 
-constexpr int kRowsPerThread = 4;  // strict repulsion: 1024 rows per block
 constexpr int kRowsPerThreadFast = 4;
+
+int device_cus() {
+  int dev = 0, cus = 0;
+  GE_HIP(hipGetDevice(&dev));
+  GE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return cus > 0 ? cus : 256;
+}
 
 template <int D>
 void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const double* X,
-                      const double* dp1, double repel, double* Frep, double* Fpart) {
+                      const double* dp1, double repel, double* Frep, double* Fpart, int cus) {
   const int rows = re - rb;
   if (rows <= 0) return;
   if (mode == GE_MODE_FAST) {
-    const int per = kRepThreads * kRowsPerThreadFast;
+    const int per = kFastThreads * kRowsPerThreadFast;
     const int jb = std::max(1, std::min(kFastJBlocks, (n + kTileJ - 1) / kTileJ));
     dim3 grid((rows + per - 1) / per, jb);
-    hipLaunchKernelGGL((fa_repulse_fast<D, kRowsPerThreadFast>), grid, dim3(kRepThreads), 0, s,
+    hipLaunchKernelGGL((fa_repulse_fast<D, kRowsPerThreadFast>), grid, dim3(kFastThreads), 0, s,
                        n, rb, re, X, dp1, repel, jb, Fpart);
     const int tot = rows * D;
     hipLaunchKernelGGL((fa_reduce_parts<D>), dim3((tot + 255) / 256), dim3(256), 0, s, rows, jb,
                        Fpart, Frep);
     return;
   }
-  const int per = kRepThreads * kRowsPerThread;
-  dim3 grid((rows + per - 1) / per);
+  // one block per CU, rows split evenly (rounded to whole 64-row wave slots)
+  const int blocks = std::max(1, std::min(cus, (rows + 63) / 64));
+  int per = (rows + blocks - 1) / blocks;
+  per = (per + 63) / 64 * 64;
+  const int nb = (rows + per - 1) / per;
   if (repel == 1.0)
-    hipLaunchKernelGGL((fa_repulse_strict<D, kRowsPerThread, true>), grid, dim3(kRepThreads), 0,
-                       s, n, rb, re, X, dp1, repel, Frep);
+    hipLaunchKernelGGL((fa_repulse_strict<D, true>), dim3(nb), dim3(kRepThreads), 0, s, n, rb, re,
+                       per, X, dp1, repel, Frep);
   else
-    hipLaunchKernelGGL((fa_repulse_strict<D, kRowsPerThread, false>), grid, dim3(kRepThreads),
-                       0, s, n, rb, re, X, dp1, repel, Frep);
+    hipLaunchKernelGGL((fa_repulse_strict<D, false>), dim3(nb), dim3(kRepThreads), 0, s, n, rb,
+                       re, per, X, dp1, repel, Frep);
 }
 
 template <int D>
@@ -452,6 +477,7 @@ struct ge_fa_plan {
   ge_fa_params p{};
   ge::FaConst c{};
   ge::DevBuf<double> dp1, frep, fprev, fpart;
+  int cus = 256;
   bool profiling = false;
   std::vector<hipEvent_t> events;  // 3 per timed step
   size_t next_event = 0;
@@ -461,6 +487,7 @@ namespace ge {
 
 static void plan_init(ge_fa_plan* pl) {
   const int rows = pl->re - pl->rb;
+  pl->cus = device_cus();
   pl->dp1.alloc(pl->n);
   pl->frep.alloc((size_t)std::max(rows, 1) * pl->dim);
   pl->fprev.alloc((size_t)std::max(rows, 1) * pl->dim);
@@ -491,7 +518,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   dispatch_dim(pl->dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
     launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
-                        pl->frep.p, pl->fpart.p);
+                        pl->frep.p, pl->fpart.p, pl->cus);
     if (ev) GE_HIP(hipEventRecord(ev[1], s));
     launch_attract<D>(s, pl->rb, pl->re, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
                       pl->fprev.p, xn, pl->c);

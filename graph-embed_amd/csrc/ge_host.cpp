@@ -15,7 +15,10 @@
 //     reference's.
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <limits>
@@ -139,12 +142,20 @@ ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, dou
     h->indices.push_back(std::move(ix));
   };
 
+  const bool prof = std::getenv("GE_PROFILE_PARTITION") != nullptr;
+  double t_scan = 0, t_resolve = 0, t_merge = 0, t_snap = 0;
+  int rounds = 0;
+  long long scanned = 0;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
   int M_prev = M;
   do {
+    ++rounds;
     std::vector<std::pair<int, int>> merges;
     double dQ = 0.0;
     for (int pass = 0; pass < matching; ++pass) {
       const int na = (int)alive.size();
+      auto t0 = now();
 #pragma omp parallel for schedule(dynamic, 512)
       for (int x = 0; x < na; ++x) {  // match scan (:1703-1726)
         const int i = alive[x];
@@ -164,6 +175,10 @@ ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, dou
         best[i] = top;
         arg[i] = who;
       }
+      auto t1 = now();
+      t_scan += secs(t0, t1);
+      if (prof)
+        for (int x = 0; x < na; ++x) scanned += !(busy[alive[x]] && best[alive[x]] != -inf);  // reference
       for (int x = 0; x < na; ++x) {  // greedy resolve (:1728-1753)
         const int i = alive[x];
         if (busy[i]) continue;
@@ -177,7 +192,9 @@ ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, dou
         busy[i] = busy[j] = 1;
         dQ += best[i];
       }
+      t_resolve += secs(t1, now());
     }
+    auto t2 = now();
     for (const auto& mg : merges) {  // contraction (:1756-1779)
       const int keep = mg.first, gone = mg.second;
       for (const auto& kv : adj[gone]) {
@@ -195,6 +212,8 @@ ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, dou
     }
     Q += dQ;
     M_prev = M;
+    auto t3 = now();
+    t_merge += secs(t2, t3);
     if (1.0 * M / N <= cf) {  // snapshot (:1797-1815)
       snap();
       basis = alive;
@@ -211,8 +230,12 @@ ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, dou
       busy[keep] = 0;
       M -= 1;
     }
+    t_snap += secs(t3, now());
   } while (1.0 * M / M_prev < stall);
   snap();
+  if (prof)
+    std::fprintf(stderr, "partition: %d rounds, scan %.3fs (%lld row scans) resolve %.3fs "
+                 "merge %.3fs snap+pop %.3fs\n", rounds, t_scan, scanned, t_resolve, t_merge, t_snap);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;
     std::cout << "level 0: " << n << " aggregates" << std::endl;

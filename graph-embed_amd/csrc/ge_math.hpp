@@ -67,6 +67,18 @@ __device__ __forceinline__ double div_by(double num, double den, const Recip& rc
   return __builtin_amdgcn_div_fixup(f, den, num);
 }
 
+// div_by without the final v_div_fixup.  In-domain the fixup is the identity
+// on every nonzero quotient (it only re-applies the sign and resolves zero,
+// inf, NaN and over/underflow operands), so the bits equal `/` whenever
+// num != 0; for num == +-0 the result is a zero whose sign may differ from `/`.
+// Only used for terms that are added to a running force sum, which is never
+// -0 (ge_fa.hip), so a zero of either sign leaves the sum unchanged.
+__device__ __forceinline__ double div_by_nz(double num, const Recip& rc) {
+  const double q = num * rc.y;
+  const double rem = __builtin_fma(-rc.ds, q, num);
+  return __builtin_fma(rem, rc.y, q);
+}
+
 // sqrt(s) for s in [2^-767, 2^1000]: the compiler's correctly rounded f64
 // sqrt expansion (LLVM AMDGPU lowerFSQRTF64: rsq + Goldschmidt refinement)
 // with its rescaling of s < 2^-767 and its zero / +inf select removed -- both

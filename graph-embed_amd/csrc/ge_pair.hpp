@@ -74,13 +74,14 @@ __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __
   double cij = dip1 * djp1;
   if (!REPEL_ONE) cij = cij * repel;
   if (SHARED) {
-    // in-domain: s == 0 or s >= 2^-504, deg+1 and repel in [2^-60, 2^60]
-    const double dis = clamp_eps(s == 0.0 ? 0.0 : sqrt_normal(s));
+    // In-domain s is 0 or >= 2^-504, so sqrt_normal(max(s, 2^-504)) is exact
+    // for s > 0 and < eps for s == 0; max(dis, eps) is the clamp (no NaN here).
+    const double dis = fmax(sqrt_normal(fmax(s, 0x1p-504)), kFaEps);
     const double dd = dis * dis;
-    const double val = div_by(cij, dd, recip_of(dd));
+    const double val = div_by_nz(cij, recip_of(dd));  // cij > 0 in-domain
     const Recip rc = recip_of(dis);
 #pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by(e[k], dis, rc) * val;
+    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by_nz(e[k], rc) * val;
   } else {
     const double dis = clamp_eps(sqrt(s));
     const double val = cij / (dis * dis);

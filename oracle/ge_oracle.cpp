@@ -187,6 +187,27 @@ int orc_fa_forces_rows(int n, const int* I, const int* J, const double* D, int d
   return 0;
 }
 
+int orc_fa_step_rows(int n, const int* I, const int* J, const double* D, int dim,
+                     const double* X, const double* deg, int rb, int re, const orc_fa_params* p,
+                     double* Fprev, double* Xn, int nthreads) {
+  if (dim < 1 || dim > kMaxDim) return 1;
+  set_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int i = rb; i < re; ++i) {
+    double F[kMaxDim];
+    fa_force_row(i, n, I, J, D, dim, X, deg, *p, F);
+    double x[kMaxDim];
+    for (int k = 0; k < dim; ++k) x[k] = X[(size_t)i * dim + k];
+    double* fp = Fprev + (size_t)(i - rb) * dim;
+    fa_update_vertex(x, F, fp, dim, *p, false);
+    for (int k = 0; k < dim; ++k) {
+      Xn[(size_t)i * dim + k] = x[k];
+      fp[k] = F[k];
+    }
+  }
+  return 0;
+}
+
 int orc_force_atlas(int n, const int* I, const int* J, const double* D, int dim,
                     double* X, int init_random, unsigned seed, int iterations,
                     const orc_fa_params* pp, int nthreads) {

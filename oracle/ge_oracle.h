@@ -58,6 +58,15 @@ int orc_fa_forces_rows(int n, const int* indptr, const int* indices, const doubl
                        int row_begin, int row_end, const orc_fa_params* p,
                        double* forces_out, int nthreads);
 
+/* One forceAtlas iteration for rows [row_begin,row_end) only (the loop body
+ * of include/forceatlas.hpp:146-269 restricted to a row shard): reads all of
+ * coords, updates fprev_rows ((row_end-row_begin)*dim, in/out) and writes rows
+ * [row_begin,row_end) of coords_next. */
+int orc_fa_step_rows(int n, const int* indptr, const int* indices, const double* data, int dim,
+                     const double* coords, const double* deg, int row_begin, int row_end,
+                     const orc_fa_params* p, double* fprev_rows, double* coords_next,
+                     int nthreads);
+
 /* deg[i] of include/forceatlas.hpp:127-140. */
 void orc_degrees(int n, const int* indptr, const double* data, int use_weights, double* deg);
 

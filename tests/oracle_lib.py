@@ -44,6 +44,9 @@ def lib():
         L.orc_fa_forces_rows.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _f64p,
                                          _f64p, ctypes.c_int, ctypes.c_int,
                                          ctypes.POINTER(FaParams), _f64p, ctypes.c_int]
+        L.orc_fa_step_rows.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _f64p,
+                                       _f64p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(FaParams), _f64p, _f64p, ctypes.c_int]
         L.orc_force_atlas_ml.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _i32p,
                                          _i32p, _i32p, _f64p, _f64p, _f64p, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_uint, ctypes.POINTER(FaParams),
@@ -125,6 +128,17 @@ def fa_forces_rows(A, coords, deg, rb, re, nthreads=0, **kw):
                                   out.reshape(-1), nthreads)
     assert rc == 0
     return out
+
+
+def fa_step_rows(A, coords, deg, rb, re, fprev_rows, coords_next, nthreads=0, **kw):
+    """One iteration for a row shard; fprev_rows and coords_next are updated in place."""
+    ip, ix, dx = _csr(A)
+    p = params(**kw)
+    rc = lib().orc_fa_step_rows(len(ip) - 1, ip, ix, dx, coords.shape[1],
+                                np.ascontiguousarray(coords).reshape(-1), deg, rb, re,
+                                ctypes.byref(p), fprev_rows.reshape(-1), coords_next.reshape(-1),
+                                nthreads)
+    assert rc == 0
 
 
 def force_atlas_ml(A, PT, vertex_A, coords_A, r_A, dim, iterations=100, seed=0, nthreads=0,

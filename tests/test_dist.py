@@ -1,0 +1,71 @@
+"""Multi-rank forceAtlas on CPU (gloo, world_size 2 and 3): the row-sharded
+driver used by bench.py (ge_amd.dist) with each rank's rows computed by the
+oracle must reproduce the single-process iteration bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import graphs as G
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, A, X0, iters, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle_lib as O
+    from ge_amd.dist import ShardedForceAtlas
+    n, dim = X0.shape
+    deg = O.degrees(A)
+    state = {}
+
+    def step_rows(cur, nxt, rb, re):
+        if "fprev" not in state:
+            state["fprev"] = np.zeros((re - rb, dim))
+        xn = nxt.numpy()
+        O.fa_step_rows(A, np.ascontiguousarray(cur.numpy()[:n]), deg, rb, re, state["fprev"],
+                       xn, nthreads=1)
+
+    drv = ShardedForceAtlas(n, world, rank, step_rows)
+    cur = torch.zeros((drv.padded_rows, dim), dtype=torch.float64)
+    cur[:n] = torch.from_numpy(X0)
+    nxt = torch.zeros_like(cur)
+    for _ in range(iters):
+        drv.step(cur, nxt)
+        cur, nxt = nxt, cur
+    if rank == 0:
+        np.save(out_path, cur[:n].numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_force_atlas_matches_single_process(oracle, tmp_path, world):
+    A = G.largest_component(G.rmat(700, 5000, seed=17))
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=5)
+    out = str(tmp_path / "x.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), A, X0, 7, out), nprocs=world,
+                       join=True, start_method="spawn")
+    got = np.load(out)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=7)
+    assert np.array_equal(got, want)
+
+
+def test_row_shards_cover_exactly():
+    from ge_amd.dist import row_shards
+    for n in (1, 7, 1000, 1000001):
+        for world in (1, 2, 3, 8):
+            chunk, sh = row_shards(n, world)
+            assert sh[0][0] == 0 and sh[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+            assert chunk * world >= n
