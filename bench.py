@@ -48,6 +48,13 @@ def parse():
     ap.add_argument("--mode", choices=["strict", "fast"], default="strict")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+                    help="c2: single-level forceAtlas (configs[1]); c3: multilevel level-0 "
+                         "forceAtlasMultilevel on the R-MAT LCC hierarchy (configs[2])")
+    ap.add_argument("--levels", type=int, default=4)
+    ap.add_argument("--ml-iterations", type=int, default=100)
+    ap.add_argument("--end-to-end", action="store_true",
+                    help="c3: also time partition::embed over the whole hierarchy")
     return ap.parse_args()
 
 
@@ -108,6 +115,137 @@ def cpu_baseline(A, X0, dim, seconds, rank):
             "seconds_per_iteration": per_iter}
 
 
+def cpu_baseline_ml(L, PT, vA, cA, rA, dim, seconds, rank):
+    """Oracle forceAtlasMultilevel on a bounded sample of aggregates (every k-th
+    aggregate), 1 iteration, scaled by the pair+edge cost of the full level."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    oracle_lib.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    pip, pix = np.asarray(PT[0]), np.asarray(PT[1])
+    s = np.diff(pip).astype(np.float64)
+    deg = np.diff(np.asarray(L[0])).astype(np.float64)
+    row_edges = np.add.reduceat(deg[pix], pip[:-1]) if len(pix) else np.zeros(len(s))
+    cost = s * (s - 1) + row_edges
+    def run(stride):
+        sel = np.arange(0, len(s), stride)
+        sizes = np.diff(pip)[sel]
+        sip = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+        six = np.concatenate([pix[pip[a]:pip[a + 1]] for a in sel]).astype(np.int32)
+        t0 = time.perf_counter()
+        oracle_lib.force_atlas_ml(L, (sip, six), vA, cA, rA, dim, iterations=1, seed=1,
+                                  nthreads=threads)
+        return time.perf_counter() - t0, cost[sel].sum()
+    stride = 64
+    t, c = run(stride)
+    stride = max(1, int(stride * t / seconds)) if t > 0 else 1
+    t, c = run(stride)
+    per_iter = t * cost.sum() / c
+    log(rank, f"cpu baseline (multilevel): stride {stride}, {t:.2f}s on {threads} threads "
+              f"-> {per_iter:.2f}s/iteration")
+    return {"value": 1.0 / per_iter, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"oracle forceAtlasMultilevel, 1 iteration over every {stride}-th aggregate "
+                      f"of level 0 ({t:.1f}s, OpenMP {threads} threads), scaled by the "
+                      f"pair+edge cost of the whole level",
+            "seconds_per_iteration": per_iter}
+
+
+def run_c3(args, rank, world, local, dev):
+    """configs[2] (C3): R-MAT 1M draw -> LCC -> partition(A, 0.125), first 4 P_T
+    (examples/embedder.cpp:189-192 pattern) -> P^T A P per level on the device.
+    One step = one forceAtlasMultilevel call on level 0 (100 iterations,
+    src/embed.cpp:793); value = level-0 iterations/s."""
+    import torch
+    import ge_amd as ge
+    t0 = time.perf_counter()
+    A = ge.rmat_csr(args.n, args.draws, seed=args.seed)
+    L = ge.largest_component(A)
+    t_gen = time.perf_counter() - t0
+    n0, nnz0 = len(L[0]) - 1, len(L[1])
+    t0 = time.perf_counter()
+    hier = ge.partition(L, 0.125)[:args.levels]
+    t_part = time.perf_counter() - t0
+    log(rank, f"LCC n={n0} nnz={nnz0} (gen {t_gen:.1f}s), partition {t_part:.1f}s, levels "
+              f"{[h[2] for h in hier]}")
+    ctx = ge.Context(local)
+    t0 = time.perf_counter()
+    As = [L]
+    for PT in hier:
+        As.append(ctx.ptap(As[-1], PT))
+    t_ptap = time.perf_counter() - t0
+    PT = hier[0]
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = ge.uniform_stream(args.seed + 1, m * args.dim).reshape(m, args.dim)
+    rA = 0.01 + 0.19 * (ge.uniform_stream(args.seed + 2, m) + 1.0) / 2.0
+    init = ge.uniform_stream(args.seed, n0 * args.dim)  # reference draw order
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d = dict(ip=T(L[0]), ix=T(L[1]), dx=T(L[2]), pip=T(PT[0]), pix=T(PT[1]), vA=T(vA),
+             cA=T(cA), rA=T(rA), init=T(init))
+    X = torch.zeros((n0, args.dim), dtype=torch.float64, device=dev)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    plan = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
+                       PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
+                       args.dim, iterations=args.ml_iterations)
+    run = lambda: plan.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(),  # noqa
+                           X.data_ptr())
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    plan.set_profiling(True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        run()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    run_ms = e0.elapsed_time(e1) / args.steps
+    res_ms, str_ms, _ = plan.kernel_ms()
+    finite = bool(torch.isfinite(X).all().item())
+    sizes = np.diff(PT[0]).astype(np.float64)
+    pairs = float((sizes * (sizes - 1)).sum())
+    flops = FLOPS_PER_PAIR * pairs * args.ml_iterations
+    its = args.steps * args.ml_iterations / elapsed
+    tflops = flops / (run_ms * 1e-3) / 1e12
+    result = {
+        "metric": METRIC, "value": its, "unit": "iterations/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "C3 (BASELINE.json configs[2]): level-0 forceAtlasMultilevel "
+                               f"({args.ml_iterations} iterations per step) on the LCC of a "
+                               f"Graph500 R-MAT ({args.n} ids, {args.draws} draws), "
+                               "partition(A, 0.125) first 4 levels, strict fp64",
+                   "n": n0, "nnz": nnz0, "aggregates": m, "dim": args.dim,
+                   "levels": [h[2] for h in hier], "parallelism": "aggregates1"},
+        "edges_per_s": nnz0 * its,
+        "pair_interactions_per_s": pairs * its,
+        "finite": finite,
+        "setup_seconds": {"graph": t_gen, "partition_host": t_part, "ptap_device": t_ptap},
+        "roofline": {"kernel": "faml_resident + faml_huge (in-aggregate all-pairs, fp64)",
+                     "bound": "mfma", "pipe": "fp64 VALU (dense FP64 peak 78.6 TFLOP/s, spec)",
+                     "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None,
+                     "flops_per_launch": flops, "avg_launch_ms": run_ms,
+                     "resident_ms": res_ms, "streamed_ms": str_ms},
+    }
+    if args.end_to_end:
+        t0 = time.perf_counter()
+        Xe = ctx.embed(As, hier, args.dim, seed=args.seed)
+        result["embed_seconds_end_to_end"] = time.perf_counter() - t0
+        result["embed_finite"] = bool(np.isfinite(Xe).all())
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_ml(L, PT, vA, cA, rA, args.dim,
+                                                 args.cpu_baseline_seconds, rank)
+        result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
+    plan.close()
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -120,6 +258,11 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.workload == "c3":
+        run_c3(args, rank, world, local, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     import ge_amd as ge
 

@@ -507,25 +507,59 @@ void build_packs(const std::vector<int>& ids, const int* h_pt_ip, int cap, int m
 
 }  // namespace
 
-void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
-                     int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
-                     const int* d_vA, const double* d_cA, const double* d_rA,
-                     const double* d_init, double* d_x, int dim, int iterations,
-                     const ge_fa_params& p) {
-  hipStream_t st = ctx->stream;
-  const int N = h_pt_ip[m];
-  GE_REQUIRE(N == n, "P_T must have one entry per fine vertex");
-  const MlConst c = make_fa_const(p);
+}  // namespace ge
 
-  // bucket aggregates by size (largest first inside each bucket)
-  std::vector<int> small, mid, large, huge;
-  for (int a = 0; a < m; ++a) {
+// ---------------------------------------------------------------------------
+// plan: bucketing, pack tables and scratch built once per (graph, P_T) level
+
+struct ge_faml_plan {
+  ge_ctx* ctx = nullptr;
+  int n = 0, m = 0, dim = 0, iterations = 0;
+  const int *ip = nullptr, *ix = nullptr, *pt_ip = nullptr, *pt_ix = nullptr, *vA = nullptr;
+  const double* dx = nullptr;
+  ge::FaConst c{};
+  int ns = 0, nm = 0, nl = 0, nb = 0, nhuge = 0;
+  size_t off_m = 0, off_l = 0;
+  ge::DevBuf<int> pos, order, beg, blk_agg, blk_li, huge;
+  ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
+  // the size classes are independent: streamed path, large, mid and small
+  // packs each run on their own stream and join the context stream at the end
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[3] = {nullptr, nullptr, nullptr};
+  bool profiling = false;
+  std::vector<hipEvent_t> ev;  // 4 per timed run: start, resident end, streamed start/end
+  size_t next_ev = 0;
+};
+
+namespace ge {
+
+static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1) {
+  hipStream_t st = pl->ctx->stream;
+  const int dim = pl->dim;
+  // Work of aggregate a per iteration ~ s^2.  Aggregates whose share would
+  // keep one CU busy for more than a quarter of the per-CU average go to the
+  // streamed path (many blocks per aggregate, one launch per iteration);
+  // the rest stay resident in LDS for all iterations.
+  double W = 0.0;
+  for (int a = a0; a < a1; ++a) {
+    const double s = h_pt_ip[a + 1] - h_pt_ip[a];
+    W += s * s;
+  }
+  int dev = 0, cus = 256;
+  GE_HIP(hipGetDevice(&dev));
+  GE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const double per_cu = W / std::max(cus, 1);
+  int split = (int)std::sqrt(per_cu / 4.0);
+  split = std::max(256, std::min(split, large_cap(dim)));
+
+  std::vector<int> small, mid, large, big;
+  for (int a = a0; a < a1; ++a) {
     const int s = h_pt_ip[a + 1] - h_pt_ip[a];
     if (s <= 0) continue;
     if (s <= 64) small.push_back(a);
     else if (s <= 256) mid.push_back(a);
-    else if (s <= large_cap(dim)) large.push_back(a);
-    else huge.push_back(a);
+    else if (s <= split) large.push_back(a);
+    else big.push_back(a);
   }
   auto by_size = [&](int x, int y) {
     const int sx = h_pt_ip[x + 1] - h_pt_ip[x], sy = h_pt_ip[y + 1] - h_pt_ip[y];
@@ -534,77 +568,249 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
   std::sort(small.begin(), small.end(), by_size);
   std::sort(mid.begin(), mid.end(), by_size);
   std::sort(large.begin(), large.end(), by_size);
+  std::sort(big.begin(), big.end(), by_size);
 
   std::vector<int> order, beg_s, beg_m, beg_l;
   build_packs(small, h_pt_ip, 64, 64, order, beg_s);
   build_packs(mid, h_pt_ip, 256, 256, order, beg_m);
   build_packs(large, h_pt_ip, large_cap(dim), 1, order, beg_l);
-
   std::vector<int> blk_agg, blk_li;
-  for (int a : huge)
+  for (int a : big)
     for (int li = 0; li < h_pt_ip[a + 1] - h_pt_ip[a]; li += kHT) {
       blk_agg.push_back(a);
       blk_li.push_back(li);
     }
-
-  DevBuf<int> d_pos(n), d_order(std::max<size_t>(order.size(), 1));
-  std::vector<int> begs;  // concatenated pack offsets
+  std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
-  const size_t off_m = begs.size();
+  pl->off_m = begs.size();
   begs.insert(begs.end(), beg_m.begin(), beg_m.end());
-  const size_t off_l = begs.size();
+  pl->off_l = begs.size();
   begs.insert(begs.end(), beg_l.begin(), beg_l.end());
-  DevBuf<int> d_beg(std::max<size_t>(begs.size(), 1));
-  DevBuf<int> d_blk_agg(std::max<size_t>(blk_agg.size(), 1)),
-      d_blk_li(std::max<size_t>(blk_li.size(), 1)), d_huge(std::max<size_t>(huge.size(), 1));
-  d_order.upload(order.data(), order.size(), st);
-  d_beg.upload(begs.data(), begs.size(), st);
-  d_blk_agg.upload(blk_agg.data(), blk_agg.size(), st);
-  d_blk_li.upload(blk_li.data(), blk_li.size(), st);
-  d_huge.upload(huge.data(), huge.size(), st);
-  DevBuf<double> Fscr((size_t)n * dim), Fprev((size_t)n * dim);
+  pl->ns = (int)beg_s.size() - 1;
+  pl->nm = (int)beg_m.size() - 1;
+  pl->nl = (int)beg_l.size() - 1;
+  pl->nb = (int)blk_agg.size();
+  pl->nhuge = (int)big.size();
 
-  hipLaunchKernelGGL(pos_of_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, d_pt_ix, d_pos.p);
-
-  dispatch_dim(dim, [&](auto Dc) {
-    constexpr int D = decltype(Dc)::value;
-    const int ns = (int)beg_s.size() - 1, nm = (int)beg_m.size() - 1, nl = (int)beg_l.size() - 1;
-    if (ns > 0)
-      hipLaunchKernelGGL((faml_resident<D, 64, 64>), dim3(ns), dim3(64), 0, st, d_order.p,
-                         d_beg.p, d_pt_ip, d_pt_ix, d_pos.p, d_vA, d_ip, d_ix, d_dx, d_cA, d_rA,
-                         d_init, Fscr.p, Fprev.p, d_x, iterations, c);
-    if (nm > 0)
-      hipLaunchKernelGGL((faml_resident<D, 256, 256>), dim3(nm), dim3(256), 0, st, d_order.p,
-                         d_beg.p + off_m, d_pt_ip, d_pt_ix, d_pos.p, d_vA, d_ip, d_ix, d_dx,
-                         d_cA, d_rA, d_init, Fscr.p, Fprev.p, d_x, iterations, c);
-    if (nl > 0)
-      hipLaunchKernelGGL((faml_resident<D, 256, large_cap(D)>), dim3(nl), dim3(256), 0, st, d_order.p,
-                         d_beg.p + off_l, d_pt_ip, d_pt_ix, d_pos.p, d_vA, d_ip, d_ix, d_dx,
-                         d_cA, d_rA, d_init, Fscr.p, Fprev.p, d_x, iterations, c);
-    GE_HIP(hipGetLastError());
-    if (!huge.empty()) {
-      DevBuf<double> Xa((size_t)n * dim), Xb((size_t)n * dim), DP(n);
-      const int nb = (int)blk_agg.size();
-      hipLaunchKernelGGL((faml_huge_init<D>), dim3(nb), dim3(kHT), 0, st, d_blk_agg.p,
-                         d_blk_li.p, d_pt_ip, d_pt_ix, d_vA, d_ip, d_ix, d_dx, d_init, Xa.p,
-                         DP.p, Fprev.p, c.use_weights);
-      double* cur = Xa.p;
-      double* nxt = Xb.p;
-      for (int it = 0; it < iterations; ++it) {
-        hipLaunchKernelGGL((faml_huge_force<D>), dim3(nb), dim3(kHT), 0, st, d_blk_agg.p,
-                           d_blk_li.p, d_pt_ip, d_pt_ix, d_pos.p, d_vA, d_ip, d_ix, d_dx, d_cA,
-                           cur, DP.p, Fscr.p, c);
-        hipLaunchKernelGGL((faml_huge_update<D>), dim3(nb), dim3(kHT), 0, st, d_blk_agg.p,
-                           d_blk_li.p, d_pt_ip, cur, nxt, Fscr.p, Fprev.p, c);
-        std::swap(cur, nxt);
-      }
-      hipLaunchKernelGGL((faml_huge_finish<D>), dim3((int)huge.size()), dim3(kHT), 0, st,
-                         d_huge.p, d_pt_ip, d_pt_ix, cur, d_cA, d_rA, d_x);
-      GE_HIP(hipGetLastError());
-      GE_HIP(hipStreamSynchronize(st));  // Xa/Xb/DP freed at scope exit
-    }
-  });
+  const int n = pl->n;
+  pl->pos.alloc(std::max(n, 1));
+  pl->order.alloc(std::max<size_t>(order.size(), 1));
+  pl->beg.alloc(std::max<size_t>(begs.size(), 1));
+  pl->blk_agg.alloc(std::max<size_t>(blk_agg.size(), 1));
+  pl->blk_li.alloc(std::max<size_t>(blk_li.size(), 1));
+  pl->huge.alloc(std::max<size_t>(big.size(), 1));
+  pl->order.upload(order.data(), order.size(), st);
+  pl->beg.upload(begs.data(), begs.size(), st);
+  pl->blk_agg.upload(blk_agg.data(), blk_agg.size(), st);
+  pl->blk_li.upload(blk_li.data(), blk_li.size(), st);
+  pl->huge.upload(big.data(), big.size(), st);
+  pl->Fscr.alloc((size_t)std::max(n, 1) * dim);
+  pl->Fprev.alloc((size_t)std::max(n, 1) * dim);
+  if (pl->nb > 0) {
+    pl->Xa.alloc((size_t)n * dim);
+    pl->Xb.alloc((size_t)n * dim);
+    pl->DP.alloc(n);
+  }
+  hipLaunchKernelGGL(pos_of_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, pl->pt_ix,
+                     pl->pos.p);
+  GE_HIP(hipGetLastError());
+  for (int k = 0; k < 3; ++k) {
+    GE_HIP(hipStreamCreateWithFlags(&pl->side[k], hipStreamNonBlocking));
+    GE_HIP(hipEventCreateWithFlags(&pl->join[k], hipEventDisableTiming));
+  }
+  GE_HIP(hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming));
   GE_HIP(hipStreamSynchronize(st));
 }
 
+static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, const double* init,
+                          double* X) {
+  hipStream_t st = pl->ctx->stream;
+  hipEvent_t* ev = nullptr;
+  if (pl->profiling) {
+    if (pl->next_ev + 4 > pl->ev.size())
+      for (int k = 0; k < 64; ++k) {
+        hipEvent_t e;
+        GE_HIP(hipEventCreate(&e));
+        pl->ev.push_back(e);
+      }
+    ev = &pl->ev[pl->next_ev];
+    pl->next_ev += 4;
+  }
+  const int iters = pl->iterations;
+  const FaConst& c = pl->c;
+  dispatch_dim(pl->dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    GE_HIP(hipEventRecord(pl->fork, st));
+    for (int k = 0; k < 3; ++k) GE_HIP(hipStreamWaitEvent(pl->side[k], pl->fork, 0));
+    if (ev) GE_HIP(hipEventRecord(ev[0], st));
+    // streamed path (side[0])
+    hipStream_t ss = pl->side[0];
+    if (ev) GE_HIP(hipEventRecord(ev[2], ss));
+    if (pl->nb > 0) {
+      hipLaunchKernelGGL((faml_huge_init<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
+                         pl->blk_li.p, pl->pt_ip, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, init,
+                         pl->Xa.p, pl->DP.p, pl->Fprev.p, c.use_weights);
+      double* cur = pl->Xa.p;
+      double* nxt = pl->Xb.p;
+      for (int it = 0; it < iters; ++it) {
+        hipLaunchKernelGGL((faml_huge_force<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
+                           pl->blk_li.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
+                           pl->dx, cA, cur, pl->DP.p, pl->Fscr.p, c);
+        hipLaunchKernelGGL((faml_huge_update<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
+                           pl->blk_li.p, pl->pt_ip, cur, nxt, pl->Fscr.p, pl->Fprev.p, c);
+        std::swap(cur, nxt);
+      }
+      hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,
+                         pl->pt_ip, pl->pt_ix, cur, cA, rA, X);
+    }
+    if (ev) GE_HIP(hipEventRecord(ev[3], ss));
+    // resident classes: large on side[1], mid on side[2], small on the context stream
+    if (pl->nl > 0)
+      hipLaunchKernelGGL((faml_resident<D, 256, large_cap(D)>), dim3(pl->nl), dim3(256), 0,
+                         pl->side[1], pl->order.p, pl->beg.p + pl->off_l, pl->pt_ip, pl->pt_ix,
+                         pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p,
+                         pl->Fprev.p, X, iters, c);
+    if (pl->nm > 0)
+      hipLaunchKernelGGL((faml_resident<D, 256, 256>), dim3(pl->nm), dim3(256), 0, pl->side[2],
+                         pl->order.p, pl->beg.p + pl->off_m, pl->pt_ip, pl->pt_ix, pl->pos.p,
+                         pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X,
+                         iters, c);
+    if (pl->ns > 0)
+      hipLaunchKernelGGL((faml_resident<D, 64, 64>), dim3(pl->ns), dim3(64), 0, st, pl->order.p,
+                         pl->beg.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
+                         pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X, iters, c);
+    for (int k = 0; k < 3; ++k) GE_HIP(hipEventRecord(pl->join[k], pl->side[k]));
+    for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(st, pl->join[k], 0));
+    if (ev) GE_HIP(hipEventRecord(ev[1], st));  // resident classes done
+    GE_HIP(hipStreamWaitEvent(st, pl->join[0], 0));
+  });
+  GE_HIP(hipGetLastError());
+}
+
+static void faml_plan_free(ge_faml_plan* pl) {
+  if (!pl) return;
+  for (int k = 0; k < 3; ++k) {
+    if (pl->side[k]) {
+      (void)hipStreamSynchronize(pl->side[k]);
+      (void)hipStreamDestroy(pl->side[k]);
+    }
+    if (pl->join[k]) (void)hipEventDestroy(pl->join[k]);
+  }
+  if (pl->fork) (void)hipEventDestroy(pl->fork);
+  for (hipEvent_t e : pl->ev) (void)hipEventDestroy(e);
+  delete pl;
+}
+
+void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
+                     int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
+                     const int* d_vA, const double* d_cA, const double* d_rA,
+                     const double* d_init, double* d_x, int dim, int iterations,
+                     const ge_fa_params& p) {
+  GE_REQUIRE(h_pt_ip[m] == n, "P_T must have one entry per fine vertex");
+  auto* pl = new ge_faml_plan();
+  try {
+    pl->ctx = ctx;
+    pl->n = n;
+    pl->m = m;
+    pl->dim = dim;
+    pl->iterations = iterations;
+    pl->ip = d_ip;
+    pl->ix = d_ix;
+    pl->dx = d_dx;
+    pl->pt_ip = d_pt_ip;
+    pl->pt_ix = d_pt_ix;
+    pl->vA = d_vA;
+    pl->c = make_fa_const(p);
+    faml_plan_build(pl, h_pt_ip, 0, m);
+    faml_plan_run(pl, d_cA, d_rA, d_init, d_x);
+    GE_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    faml_plan_free(pl);
+    throw;
+  }
+  faml_plan_free(pl);
+}
+
 }  // namespace ge
+
+extern "C" {
+
+int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
+                        int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
+                        const int* d_vA, int dim, const ge_fa_params* p, int iterations,
+                        int agg_begin, int agg_end, ge_faml_plan** out) {
+  return ge::guarded([&] {
+    GE_REQUIRE(ctx && p && out && h_pt_ip, "null argument");
+    GE_REQUIRE(dim >= 1 && dim <= 4, "dimension must be 1..4");
+    GE_REQUIRE(n > 0 && m > 0 && h_pt_ip[0] == 0 && h_pt_ip[m] == n,
+               "P_T must have one entry per fine vertex");
+    GE_REQUIRE(0 <= agg_begin && agg_begin <= agg_end && agg_end <= m, "bad aggregate range");
+    ge::DeviceGuard g(ctx);
+    auto* pl = new ge_faml_plan();
+    try {
+      pl->ctx = ctx;
+      pl->n = n;
+      pl->m = m;
+      pl->dim = dim;
+      pl->iterations = iterations;
+      pl->ip = d_ip;
+      pl->ix = d_ix;
+      pl->dx = d_dx;
+      pl->pt_ip = d_pt_ip;
+      pl->pt_ix = d_pt_ix;
+      pl->vA = d_vA;
+      pl->c = ge::make_fa_const(*p);
+      ge::faml_plan_build(pl, h_pt_ip, agg_begin, agg_end);
+    } catch (...) {
+      ge::faml_plan_free(pl);
+      throw;
+    }
+    *out = pl;
+  });
+}
+
+int ge_faml_plan_run(ge_faml_plan* pl, const double* d_cA, const double* d_rA,
+                     const double* d_init, double* d_coords) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && d_cA && d_rA && d_init && d_coords, "null argument");
+    ge::DeviceGuard g(pl->ctx);
+    ge::faml_plan_run(pl, d_cA, d_rA, d_init, d_coords);
+  });
+}
+
+int ge_faml_plan_set_profiling(ge_faml_plan* pl, int enable) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl, "null plan");
+    pl->profiling = enable != 0;
+    pl->next_ev = 0;
+  });
+}
+
+int ge_faml_plan_kernel_ms(ge_faml_plan* pl, double* resident_ms, double* streamed_ms,
+                           int* runs) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && resident_ms && streamed_ms && runs, "null argument");
+    ge::DeviceGuard g(pl->ctx);
+    GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+    double a = 0, b = 0;
+    int cnt = 0;
+    for (size_t k = 0; k + 4 <= pl->next_ev; k += 4) {
+      float t1 = 0.f, t2 = 0.f;
+      GE_HIP(hipEventElapsedTime(&t1, pl->ev[k], pl->ev[k + 1]));
+      GE_HIP(hipEventElapsedTime(&t2, pl->ev[k + 2], pl->ev[k + 3]));
+      a += t1;
+      b += t2;
+      ++cnt;
+    }
+    *resident_ms = cnt ? a / cnt : 0.0;
+    *streamed_ms = cnt ? b / cnt : 0.0;
+    *runs = cnt;
+  });
+}
+
+int ge_faml_plan_destroy(ge_faml_plan* pl) {
+  return ge::guarded([&] { ge::faml_plan_free(pl); });
+}
+
+}  // extern "C"
+

@@ -3,12 +3,7 @@
 //
 // Device work lives in ge_fa.hip / ge_faml.hip / ge_ptap.hip; this file moves
 // data, sequences levels and runs the host-resident algorithms:
-//   * partition hierarchy (src/partitioner.cpp:1550-1893): greedy modularity
-//     pair matching.  Hash-map adjacency instead of the reference's std::map:
-//     the match scan takes the largest eta with ties to the smallest neighbour
-//     id, which is exactly what the reference's ascending scan with strict `>`
-//     selects, and the contraction adds each weight once per merge in merge
-//     order, so the result is identical while every map operation is O(1).
+//   * partition hierarchy: ge_partition.cpp (incremental, bit-exact).
 //   * radius ("kinetic ball") step (src/embed.cpp:615-777) with an ordered set
 //     instead of a full re-sort after every event; the popped sequence (always
 //     the largest (time, i, j) tuple) and every time update are the
@@ -78,172 +73,6 @@ struct DevCsr {
     dx.upload(hdx, nnz, s);
   }
 };
-
-// ---------------------------------------------------------------------------
-// partition hierarchy
-
-ge_hier* partition_host(int n, const int* I, const int* J, const double* Dv, double cf,
-                        bool printing, bool positive, double stall, int matching) {
-  const double inf = std::numeric_limits<double>::infinity();
-  auto* h = new ge_hier();
-  int N = n, M = n;
-  std::vector<std::unordered_map<int, double>> adj(n);
-  std::vector<double> alpha(n);
-  double T = 0.0, self_sum = 0.0;
-#pragma omp parallel for schedule(dynamic, 256)
-  for (int i = 0; i < n; ++i) {
-    adj[i].reserve((size_t)(I[i + 1] - I[i]) * 2);
-    double s = 0.0;
-    for (int e = I[i]; e < I[i + 1]; ++e) {
-      if (J[e] != i) adj[i].emplace(J[e], Dv[e]);  // first occurrence wins, as map::insert
-      s += Dv[e];
-    }
-    alpha[i] = s;
-  }
-  for (int i = 0; i < n; ++i)
-    for (int e = I[i]; e < I[i + 1]; ++e) {
-      if (J[e] == i) self_sum += Dv[e];
-      T += Dv[e];
-    }
-  for (int i = 0; i < n; ++i) alpha[i] /= T;
-  double Q = self_sum / T;  // reported when printing (:1601-1605)
-  for (int i = 0; i < n; ++i) Q += -alpha[i] * alpha[i];
-
-  std::vector<int> basis(n), alive(n), slot(n), up(n);
-  std::iota(basis.begin(), basis.end(), 0);
-  alive = slot = up = basis;
-  std::vector<double> best(n, -inf);
-  std::vector<int> arg(n, 0);
-  std::vector<char> busy(n, 0);
-
-  auto root = [&](int x) {
-    int r = x;
-    while (up[r] != r) r = up[r];
-    while (up[x] != r) {
-      int nx = up[x];
-      up[x] = r;
-      x = nx;
-    }
-    return r;
-  };
-  auto snap = [&]() {
-    std::vector<int> cnt(M + 1, 0), rowof(basis.size());
-    for (size_t y = 0; y < basis.size(); ++y) {
-      rowof[y] = slot[root(basis[y])];
-      cnt[rowof[y] + 1]++;
-    }
-    for (int r = 0; r < M; ++r) cnt[r + 1] += cnt[r];
-    std::vector<int> ix(basis.size());
-    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
-    for (size_t y = 0; y < basis.size(); ++y) ix[fill[rowof[y]]++] = (int)y;
-    h->rows.push_back(M);
-    h->cols.push_back(N);
-    h->indptr.push_back(std::move(cnt));
-    h->indices.push_back(std::move(ix));
-  };
-
-  const bool prof = std::getenv("GE_PROFILE_PARTITION") != nullptr;
-  double t_scan = 0, t_resolve = 0, t_merge = 0, t_snap = 0;
-  int rounds = 0;
-  long long scanned = 0;
-  auto now = [] { return std::chrono::steady_clock::now(); };
-  auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
-  int M_prev = M;
-  do {
-    ++rounds;
-    std::vector<std::pair<int, int>> merges;
-    double dQ = 0.0;
-    for (int pass = 0; pass < matching; ++pass) {
-      const int na = (int)alive.size();
-      auto t0 = now();
-#pragma omp parallel for schedule(dynamic, 512)
-      for (int x = 0; x < na; ++x) {  // match scan (:1703-1726)
-        const int i = alive[x];
-        if (busy[i] && best[i] != -inf) continue;
-        double top = -inf;
-        int who = -1;
-        const double ai = alpha[i];
-        for (const auto& kv : adj[i]) {
-          const int j = kv.first;
-          if (busy[j]) continue;
-          const double eta = 2 * (kv.second / T - ai * alpha[j]);
-          if (eta > top || (eta == top && j < who)) {
-            top = eta;
-            who = j;
-          }
-        }
-        best[i] = top;
-        arg[i] = who;
-      }
-      auto t1 = now();
-      t_scan += secs(t0, t1);
-      if (prof)
-        for (int x = 0; x < na; ++x) scanned += !(busy[alive[x]] && best[alive[x]] != -inf);  // reference
-      for (int x = 0; x < na; ++x) {  // greedy resolve (:1728-1753)
-        const int i = alive[x];
-        if (busy[i]) continue;
-        const int j = arg[i];
-        if (j == -1 || busy[j] || best[i] < best[j]) continue;
-        if (positive && !(best[i] > 0)) continue;
-        if (adj[i].size() < adj[j].size())
-          merges.emplace_back(j, i);
-        else
-          merges.emplace_back(i, j);
-        busy[i] = busy[j] = 1;
-        dQ += best[i];
-      }
-      t_resolve += secs(t1, now());
-    }
-    auto t2 = now();
-    for (const auto& mg : merges) {  // contraction (:1756-1779)
-      const int keep = mg.first, gone = mg.second;
-      for (const auto& kv : adj[gone]) {
-        const int k = kv.first;
-        adj[k].erase(gone);
-        best[k] = -inf;
-        if (k == keep) {
-          alpha[keep] = alpha[keep] + alpha[gone];
-        } else {
-          adj[keep][k] += kv.second;
-          adj[k][keep] += kv.second;
-        }
-      }
-      std::unordered_map<int, double>().swap(adj[gone]);
-    }
-    Q += dQ;
-    M_prev = M;
-    auto t3 = now();
-    t_merge += secs(t2, t3);
-    if (1.0 * M / N <= cf) {  // snapshot (:1797-1815)
-      snap();
-      basis = alive;
-      N = M;
-    }
-    for (const auto& mg : merges) {  // swap-pop + union (:1819-1834)
-      const int keep = mg.first, gone = mg.second;
-      const int s = slot[gone];
-      const int last = alive.back();
-      std::swap(alive[s], alive.back());
-      alive.pop_back();
-      slot[last] = s;
-      up[gone] = keep;
-      busy[keep] = 0;
-      M -= 1;
-    }
-    t_snap += secs(t3, now());
-  } while (1.0 * M / M_prev < stall);
-  snap();
-  if (prof)
-    std::fprintf(stderr, "partition: %d rounds, scan %.3fs (%lld row scans) resolve %.3fs "
-                 "merge %.3fs snap+pop %.3fs\n", rounds, t_scan, scanned, t_resolve, t_merge, t_snap);
-  if (printing) {  // :1880-1889
-    std::cout << "modularity: " << Q << std::endl;
-    std::cout << "level 0: " << n << " aggregates" << std::endl;
-    for (size_t l = 0; l < h->rows.size(); ++l)
-      std::cout << "level " << l + 1 << ": " << h->rows[l] << " aggregates" << std::endl;
-  }
-  return h;
-}
 
 // ---------------------------------------------------------------------------
 // radius step (src/embed.cpp:615-777)
@@ -575,7 +404,8 @@ int ge_partition(ge_ctx* ctx, int n, const int* ip, const int* ix, const double*
     GE_REQUIRE(!merge_leaves, "mergeLeaves is not supported (off by default; buggy in the "
                               "reference, src/partitioner.cpp:1680)");
     ge::check_csr(n, ip, ix, dx);
-    *out = ge::partition_host(n, ip, ix, dx, cf, printing != 0, positive != 0, stall, matching);
+    *out = ge::partition_incremental(n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
+                                     matching);
   });
 }
 

@@ -132,6 +132,8 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
                      const int* d_vA, const double* d_cA, const double* d_rA,
                      const double* d_init, double* d_x, int dim, int iterations,
                      const ge_fa_params& p);
+ge_hier* partition_incremental(int n, const int* I, const int* J, const double* Dv, double cf,
+                               bool printing, bool positive, double stall, int matching);
 void ptap_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
                  int nnz, int m, const int* d_pt_ip, const int* d_pt_ix, ge_csr* out);
 

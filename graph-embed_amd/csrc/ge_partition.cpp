@@ -1,0 +1,376 @@
+// ge_partition.cpp -- the coarsening hierarchy (partition::partition,
+// src/partitioner.cpp:1550-1893), bit-exact, with work proportional to what
+// changes per round instead of to the graph.
+//
+// The reference runs rounds of greedy modularity pair matching until a round
+// merges nothing.  Rounds grow with the largest aggregate (a hub absorbs one
+// neighbour per round: 1255 rounds for a 148K-vertex R-MAT LCC), and every
+// round rescans every alive vertex's adjacency (std::map) twice.  Here:
+//
+//  * Adjacency: one open-addressing hash table per vertex (O(1) find/insert/
+//    erase).  The scan takes the largest eta with ties to the smallest
+//    neighbour id -- exactly what the reference's ascending map walk with
+//    strict `>` selects (:1710-1720) -- so iteration order does not matter.
+//    The contraction adds each weight once per merge, in merge order, like
+//    `a[i'][k] += w; a[k][i'] += w` (:1772-1773).
+//  * Scan skipping: a vertex is rescanned only if an input of its scan changed
+//    since its last scan (its neighbours or their weights, alpha of it or of a
+//    neighbour, a neighbour's busy flag).  A clean vertex would recompute the
+//    same (max_eta, max_ind), so best/arg stay identical to the reference's
+//    arrays at every step.  The reference's own skip rule
+//    (`notouch[i] && max_eta[i] != -inf`, :1706) is applied on top.
+//  * Resolve: only vertices with a usable candidate (max_ind != -1, and
+//    max_eta > 0 under positiveMerging) can merge (:1730-1735).  They are kept
+//    in a bitmap over `used` slots and visited in slot order -- the reference's
+//    `used` order -- so the greedy decisions are the same.
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "ge_internal.hpp"
+
+namespace ge {
+namespace {
+
+// Open-addressing int -> double map (linear probing, tombstones).
+class NbrMap {
+ public:
+  static constexpr int kEmpty = -1, kTomb = -2;
+  int size() const { return live_; }
+
+  void reserve(int want) {
+    int cap = 4;
+    while (cap < 2 * want) cap <<= 1;
+    if (cap > (int)keys_.size()) rehash(cap);
+  }
+  // first insertion wins (std::map::insert semantics)
+  void insert_new(int k, double v) {
+    grow_if_needed();
+    int at = probe(k);
+    if (keys_[at] == k) return;
+    place(at, k, v);
+  }
+  // m[k] += v (operator[] then +=: 0.0 + v for a new key)
+  void add(int k, double v) {
+    grow_if_needed();
+    int at = probe(k);
+    if (keys_[at] == k) {
+      vals_[at] += v;
+      return;
+    }
+    place(at, k, 0.0 + v);
+  }
+  void erase(int k) {
+    if (keys_.empty()) return;
+    const int mask = (int)keys_.size() - 1;
+    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
+      if (keys_[h] == k) {
+        keys_[h] = kTomb;
+        --live_;
+        return;
+      }
+      if (keys_[h] == kEmpty) return;
+    }
+  }
+  template <class F>
+  void for_each(F&& f) const {
+    for (size_t h = 0; h < keys_.size(); ++h)
+      if (keys_[h] >= 0) f(keys_[h], vals_[h]);
+  }
+  void clear() {
+    std::vector<int>().swap(keys_);
+    std::vector<double>().swap(vals_);
+    live_ = used_ = 0;
+  }
+
+ private:
+  static int hash(int k) { return (int)(((uint32_t)k * 2654435761u) >> 1); }
+  // slot of k if present, else the first free slot (tombstone or empty) on its chain
+  int probe(int k) const {
+    const int mask = (int)keys_.size() - 1;
+    int tomb = -1;
+    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
+      if (keys_[h] == k) return h;
+      if (keys_[h] == kTomb) {
+        if (tomb < 0) tomb = h;
+      } else if (keys_[h] == kEmpty) {
+        return tomb >= 0 ? tomb : h;
+      }
+    }
+  }
+  void place(int at, int k, double v) {
+    if (keys_[at] == kEmpty) ++used_;
+    keys_[at] = k;
+    vals_[at] = v;
+    ++live_;
+  }
+  void grow_if_needed() {
+    if (keys_.empty()) {
+      rehash(4);
+    } else if (2 * (used_ + 1) > (int)keys_.size()) {
+      int cap = (int)keys_.size();
+      while (4 * (live_ + 1) > cap) cap <<= 1;  // keep load <= 1/4 after rehash
+      rehash(std::max(cap, 4));
+    }
+  }
+  void rehash(int cap) {
+    std::vector<int> ok(cap, kEmpty);
+    std::vector<double> ov(cap);
+    const int mask = cap - 1;
+    for (size_t h = 0; h < keys_.size(); ++h) {
+      if (keys_[h] < 0) continue;
+      int at = hash(keys_[h]) & mask;
+      while (ok[at] != kEmpty) at = (at + 1) & mask;
+      ok[at] = keys_[h];
+      ov[at] = vals_[h];
+    }
+    keys_.swap(ok);
+    vals_.swap(ov);
+    used_ = live_;
+  }
+  std::vector<int> keys_;
+  std::vector<double> vals_;
+  int live_ = 0, used_ = 0;
+};
+
+struct Bitmap {
+  std::vector<uint64_t> w;
+  void resize(size_t bits) { w.assign((bits + 63) / 64, 0); }
+  void set(int i) { w[i >> 6] |= 1ull << (i & 63); }
+  void clr(int i) { w[i >> 6] &= ~(1ull << (i & 63)); }
+  bool get(int i) const { return (w[i >> 6] >> (i & 63)) & 1ull; }
+};
+
+}  // namespace
+
+ge_hier* partition_incremental(int n, const int* I, const int* J, const double* Dv, double cf,
+                               bool printing, bool positive, double stall, int matching) {
+  const double inf = std::numeric_limits<double>::infinity();
+  const bool prof = std::getenv("GE_PROFILE_PARTITION") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  const auto t_start = now();
+  auto* h = new ge_hier();
+  int N = n, M = n;
+
+  std::vector<NbrMap> adj(n);
+  std::vector<double> alpha(n);
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int i = 0; i < n; ++i) {  // :1561-1577
+    adj[i].reserve(I[i + 1] - I[i]);
+    double s = 0.0;
+    for (int e = I[i]; e < I[i + 1]; ++e) {
+      if (J[e] != i) adj[i].insert_new(J[e], Dv[e]);
+      s += Dv[e];
+    }
+    alpha[i] = s;
+  }
+  double T = 0.0, self_sum = 0.0;  // :1580-1591
+  for (int i = 0; i < n; ++i)
+    for (int e = I[i]; e < I[i + 1]; ++e) {
+      if (J[e] == i) self_sum += Dv[e];
+      T += Dv[e];
+    }
+  for (int i = 0; i < n; ++i) alpha[i] /= T;
+  double Q = self_sum / T;
+  for (int i = 0; i < n; ++i) Q += -alpha[i] * alpha[i];
+
+  std::vector<int> basis(n), alive(n), slot(n), up(n);
+  std::iota(basis.begin(), basis.end(), 0);
+  alive = slot = up = basis;
+  std::vector<char> dead(n, 0), busy(n, 0), dirty(n, 1);
+  std::vector<double> best(n, -inf);
+  std::vector<int> arg(n, 0);
+  std::vector<int> work(n);  // dirty vertices
+  std::iota(work.begin(), work.end(), 0);
+  Bitmap cand;  // over `alive` slots: max_ind != -1 (and max_eta > 0 if positive)
+  cand.resize(n);
+
+  auto mark = [&](int v) {
+    if (!dirty[v]) {
+      dirty[v] = 1;
+      work.push_back(v);
+    }
+  };
+  auto mark_nbrs = [&](int v) { adj[v].for_each([&](int k, double) { mark(k); }); };
+  auto set_cand = [&](int v) {
+    const bool c = arg[v] != -1 && (!positive || best[v] > 0);
+    if (c) cand.set(slot[v]);
+    else cand.clr(slot[v]);
+  };
+  auto root = [&](int x) {
+    int r = x;
+    while (up[r] != r) r = up[r];
+    while (up[x] != r) {
+      const int nx = up[x];
+      up[x] = r;
+      x = nx;
+    }
+    return r;
+  };
+  auto snap = [&]() {  // :1797-1815 / :1840-1852 and interpolationMatrix :29-65
+    std::vector<int> cnt(M + 1, 0), rowof(basis.size());
+    for (size_t y = 0; y < basis.size(); ++y) {
+      rowof[y] = slot[root(basis[y])];
+      cnt[rowof[y] + 1]++;
+    }
+    for (int r = 0; r < M; ++r) cnt[r + 1] += cnt[r];
+    std::vector<int> ix(basis.size());
+    std::vector<int> fill(cnt.begin(), cnt.end() - 1);
+    for (size_t y = 0; y < basis.size(); ++y) ix[fill[rowof[y]]++] = (int)y;
+    h->rows.push_back(M);
+    h->cols.push_back(N);
+    h->indptr.push_back(std::move(cnt));
+    h->indices.push_back(std::move(ix));
+  };
+
+  double t_scan = 0, t_resolve = 0, t_merge = 0, t_pop = 0;
+  long long rescans = 0;
+  int rounds = 0;
+  std::vector<int> todo, keep_dirty;
+  int M_prev = M;
+  do {
+    ++rounds;
+    std::vector<std::pair<int, int>> merges;
+    double dQ = 0.0;
+    for (int pass = 0; pass < matching; ++pass) {
+      const auto t0 = now();
+      // ---- scan (:1703-1726) over the dirty vertices the reference would scan
+      todo.clear();
+      keep_dirty.clear();
+      for (int v : work) {
+        if (dead[v]) {
+          dirty[v] = 0;
+        } else if (busy[v] && best[v] != -inf) {
+          keep_dirty.push_back(v);  // not scanned this pass; stays dirty
+        } else {
+          todo.push_back(v);
+          dirty[v] = 0;
+        }
+      }
+      work.swap(keep_dirty);
+      const int nt = (int)todo.size();
+      rescans += nt;
+#pragma omp parallel for schedule(dynamic, 64)
+      for (int x = 0; x < nt; ++x) {
+        const int i = todo[x];
+        double top = -inf;
+        int who = -1;
+        const double ai = alpha[i];
+        adj[i].for_each([&](int j, double w) {
+          if (busy[j]) return;
+          const double eta = 2 * (w / T - ai * alpha[j]);
+          if (eta > top || (eta == top && j < who)) {
+            top = eta;
+            who = j;
+          }
+        });
+        best[i] = top;
+        arg[i] = who;
+      }
+      for (int x = 0; x < nt; ++x) set_cand(todo[x]);
+      const auto t1 = now();
+      t_scan += secs(t0, t1);
+      // ---- greedy resolve in `used` order (:1728-1753)
+      const int words = (int)((alive.size() + 63) / 64);
+      for (int wi = 0; wi < words; ++wi) {
+        uint64_t bits = cand.w[wi];
+        while (bits) {
+          const int x = wi * 64 + __builtin_ctzll(bits);
+          bits &= bits - 1;
+          if (x >= (int)alive.size()) break;
+          const int i = alive[x];
+          if (busy[i]) continue;
+          const int j = arg[i];
+          if (j == -1 || busy[j] || best[i] < best[j]) continue;
+          if (positive && !(best[i] > 0)) continue;
+          if (adj[i].size() < adj[j].size())
+            merges.emplace_back(j, i);
+          else
+            merges.emplace_back(i, j);
+          busy[i] = busy[j] = 1;
+          mark_nbrs(i);  // their candidate sets lost i and j
+          mark_nbrs(j);
+          dQ += best[i];
+        }
+      }
+      t_resolve += secs(t1, now());
+    }
+    // ---- contraction (:1756-1779)
+    const auto t2 = now();
+    for (const auto& mg : merges) {
+      const int keep = mg.first, gone = mg.second;
+      adj[gone].for_each([&](int k, double w) {
+        adj[k].erase(gone);
+        best[k] = -inf;
+        cand.clr(slot[k]);
+        mark(k);
+        if (k == keep) {
+          alpha[keep] = alpha[keep] + alpha[gone];
+        } else {
+          adj[keep].add(k, w);
+          adj[k].add(keep, w);
+        }
+      });
+      adj[gone].clear();
+      mark(keep);
+      mark_nbrs(keep);  // alpha[keep] changed; keep becomes a candidate again
+    }
+    Q += dQ;
+    M_prev = M;
+    const auto t3 = now();
+    t_merge += secs(t2, t3);
+    if (1.0 * M / N <= cf) {
+      snap();
+      basis = alive;
+      N = M;
+    }
+    // ---- swap-pop + union (:1819-1834); the candidate bit moves with its vertex
+    for (const auto& mg : merges) {
+      const int keep = mg.first, gone = mg.second;
+      const int s = slot[gone];
+      const int L = (int)alive.size() - 1;
+      const int last = alive[L];
+      const bool bit_last = cand.get(L);
+      std::swap(alive[s], alive[L]);
+      alive.pop_back();
+      slot[last] = s;
+      if (bit_last) cand.set(s);
+      else cand.clr(s);
+      cand.clr(L);
+      dead[gone] = 1;
+      up[gone] = keep;
+      busy[keep] = 0;
+      M -= 1;
+    }
+    t_pop += secs(t3, now());
+    if (prof && std::getenv("GE_PROFILE_ROUNDS"))
+      std::fprintf(stderr, "round %d alive %d merges %zu rescans_total %lld\n", rounds, M,
+                   merges.size(), rescans);
+  } while (1.0 * M / M_prev < stall);
+  snap();
+  if (prof)
+    std::fprintf(stderr,
+                 "partition: n=%d %d rounds %.3fs: scan %.3fs (%lld rescans) resolve %.3fs "
+                 "merge %.3fs snap+pop %.3fs\n",
+                 n, rounds, secs(t_start, now()), t_scan, rescans, t_resolve, t_merge, t_pop);
+  if (printing) {  // :1880-1889
+    std::cout << "modularity: " << Q << std::endl;
+    std::cout << "level 0: " << n << " aggregates" << std::endl;
+    for (size_t l = 0; l < h->rows.size(); ++l)
+      std::cout << "level " << l + 1 << ": " << h->rows[l] << " aggregates" << std::endl;
+  }
+  return h;
+}
+
+}  // namespace ge

@@ -90,6 +90,15 @@ _SIGS = {
     "ge_radius_step": (ctypes.c_int, [ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "ge_uniform_stream": (ctypes.c_int, [ctypes.c_uint, ctypes.c_longlong, _f64p]),
+    "ge_faml_plan_create": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _i32p,
+                                           _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(FaParams),
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(_vp)]),
+    "ge_faml_plan_run": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ge_faml_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "ge_faml_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double), _ip]),
+    "ge_faml_plan_destroy": (ctypes.c_int, [_vp]),
     "ge_selftest_math": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_ulonglong,
                                         ctypes.POINTER(ctypes.c_longlong)]),
     "ge_rmat_csr": (ctypes.c_int, [ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
@@ -233,6 +242,47 @@ class Context:
 
     def fa_plan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw):
         return FaPlan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw)
+
+
+class FamlPlan:
+    """Device-resident multilevel level (ge_faml_plan_*): P_T's indptr on the host
+    (pt_indptr_host, numpy) plus device pointers for everything else."""
+
+    def __init__(self, ctx, n, d_ip, d_ix, d_dx, pt_indptr_host, d_pt_ip, d_pt_ix, d_vA, dim,
+                 iterations=100, agg_range=None, **kw):
+        self.ctx = ctx
+        pip = np.ascontiguousarray(pt_indptr_host, dtype=np.int32)
+        m = len(pip) - 1
+        a0, a1 = agg_range if agg_range else (0, m)
+        p = params(**kw)
+        h = _vp()
+        _check(lib().ge_faml_plan_create(ctx.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip,
+                                         _vp(d_pt_ip), _vp(d_pt_ix), _vp(d_vA), dim,
+                                         ctypes.byref(p), iterations, a0, a1, ctypes.byref(h)))
+        self.h = h
+
+    def run(self, d_cA, d_rA, d_init, d_x):
+        _check(lib().ge_faml_plan_run(self.h, _vp(d_cA), _vp(d_rA), _vp(d_init), _vp(d_x)))
+
+    def set_profiling(self, on):
+        _check(lib().ge_faml_plan_set_profiling(self.h, int(on)))
+
+    def kernel_ms(self):
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        _check(lib().ge_faml_plan_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b),
+                                            ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def close(self):
+        if self.h:
+            lib().ge_faml_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class FaPlan:

@@ -23,12 +23,13 @@ def allgather_rows(x_full, chunk, rank, world):
     if world == 1:
         return
     import torch.distributed as dist
-    mine = x_full[rank * chunk:(rank + 1) * chunk]
+    # a separate send buffer keeps the collective out-of-place (chunk x d fp64)
+    mine = x_full[rank * chunk:(rank + 1) * chunk].clone()
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(x_full, mine)
     else:  # gloo: list form
         parts = list(x_full.split(chunk))
-        dist.all_gather(parts, mine.clone())
+        dist.all_gather(parts, mine)
 
 
 class ShardedForceAtlas:

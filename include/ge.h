@@ -98,6 +98,25 @@ int ge_force_atlas_ml(ge_ctx* ctx, int n, const int* indptr, const int* indices,
                       const double* r_A, double* coords, int dim, int iterations,
                       const ge_fa_params* p);
 
+/* Device-resident multilevel level (the bench and multi-GPU path).  Aggregates
+ * [agg_begin, agg_end) of P_T are processed; h_pt_indptr is a HOST copy of
+ * P_T's indptr (used to bucket aggregates by size), every other array is on the
+ * device.  Run: d_init = the n*dim draws in P_T storage order (ge_uniform_stream),
+ * d_coords receives the members' coordinates (fine-vertex order). */
+typedef struct ge_faml_plan ge_faml_plan;
+int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_indptr, const int* d_indices,
+                        const double* d_data, int m, const int* h_pt_indptr,
+                        const int* d_pt_indptr, const int* d_pt_indices, const int* d_vertex_A,
+                        int dim, const ge_fa_params* p, int iterations, int agg_begin,
+                        int agg_end, ge_faml_plan** out);
+int ge_faml_plan_run(ge_faml_plan* plan, const double* d_coords_A, const double* d_r_A,
+                     const double* d_init, double* d_coords);
+int ge_faml_plan_set_profiling(ge_faml_plan* plan, int enable);
+/* Average device ms of the resident (LDS) kernels and of the streamed path per run. */
+int ge_faml_plan_kernel_ms(ge_faml_plan* plan, double* resident_ms, double* streamed_ms,
+                           int* runs);
+int ge_faml_plan_destroy(ge_faml_plan* plan);
+
 /* ---- coarsening hierarchy ----
  * Replaces std::vector<SparseMatrix> partition::partition(A, coarseningFactor,
  * printing, positiveMerging, stallStopThreshold, matchingIterations,

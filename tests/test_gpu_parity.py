@@ -226,3 +226,31 @@ def test_embed_rmat_vs_oracle(ctx, oracle):
     want = oracle.embed(As, hier, 3, seed=9, base_iterations=20000)
     assert np.array_equal(X, want)
     assert np.isfinite(X).all()
+
+
+def test_faml_plan_device_resident_and_ranges(ctx, oracle):
+    """ge_faml_plan_* (device pointers, the bench / multi-GPU path) on a full
+    level and on two aggregate ranges that together cover it."""
+    torch = pytest.importorskip("torch")
+    A = G.largest_component(G.rmat(5000, 40000, seed=99))
+    n = len(A[0]) - 1
+    PT = oracle.partition(A, 0.125)[0]
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = G.random_coords(m, 3, seed=3)
+    rA = np.random.RandomState(4).uniform(0.05, 0.3, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=25, seed=8)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d = [T(A[0]), T(A[1]), T(A[2]), T(PT[0]), T(PT[1]), T(vA), T(cA), T(rA),
+         T(ge.uniform_stream(8, n * 3))]
+    ptr = [t.data_ptr() for t in d]
+    for ranges in ([(0, m)], [(0, m // 3), (m // 3, m)]):
+        X = torch.zeros((n, 3), dtype=torch.float64, device=dev)
+        for rg in ranges:
+            plan = ge.FamlPlan(ctx, n, ptr[0], ptr[1], ptr[2], PT[0], ptr[3], ptr[4], ptr[5], 3,
+                               iterations=25, agg_range=rg)
+            plan.run(ptr[6], ptr[7], ptr[8], X.data_ptr())
+            ctx.sync()
+            plan.close()
+        assert np.array_equal(X.cpu().numpy(), want)
