@@ -53,6 +53,8 @@ def parse():
                          "forceAtlasMultilevel on the R-MAT LCC hierarchy (configs[2])")
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--ml-iterations", type=int, default=100)
+    ap.add_argument("--sweep-slots", action="store_true",
+                    help="c3: also time the streamed path at 1, 2 and 4 row slots per lane")
     ap.add_argument("--end-to-end", action="store_true",
                     help="c3: also time partition::embed over the whole hierarchy")
     return ap.parse_args()
@@ -183,7 +185,11 @@ def run_c3(args, rank, world, local, dev):
     d = dict(ip=T(L[0]), ix=T(L[1]), dx=T(L[2]), pip=T(PT[0]), pix=T(PT[1]), vA=T(vA),
              cA=T(cA), rA=T(rA), init=T(init))
     X = torch.zeros((n0, args.dim), dtype=torch.float64, device=dev)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    # a dedicated (non-null) stream made torch's current one: the library launches
+    # on it, and torch events and collectives order against it
+    work = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(work)
+    ctx.set_stream(work.cuda_stream)
     plan = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
                        PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
                        args.dim, iterations=args.ml_iterations)
@@ -241,6 +247,20 @@ def run_c3(args, rank, world, local, dev):
                                                  args.cpu_baseline_seconds, rank)
         result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
     plan.close()
+    if args.sweep_slots:  # streamed-path row slots per lane (tuning aid, stderr only)
+        for R in (1, 2, 4):
+            os.environ["GE_FAML_R"] = str(R)
+            p2 = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
+                             PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
+                             args.dim, iterations=args.ml_iterations)
+            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            torch.cuda.synchronize(dev)
+            log(rank, f"sweep R={R}: {1e3 * (time.perf_counter() - t0):.1f} ms per call")
+            p2.close()
+        os.environ.pop("GE_FAML_R")
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -284,7 +304,11 @@ def main():
     xb = torch.zeros_like(xa)
 
     ctx = ge.Context(local)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    # a dedicated (non-null) stream made torch's current one: the library launches
+    # on it, and torch events and collectives order against it
+    work = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(work)
+    ctx.set_stream(work.cuda_stream)
     mode = ge.MODE_FAST if args.mode == "fast" else ge.MODE_STRICT
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), args.dim, rb, re,
                        mode=mode)
@@ -378,6 +402,20 @@ def main():
         result["cpu_baseline"] = cpu_baseline(A, X0, args.dim, args.cpu_baseline_seconds, rank)
         result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
     plan.close()
+    if args.sweep_slots:  # streamed-path row slots per lane (tuning aid, stderr only)
+        for R in (1, 2, 4):
+            os.environ["GE_FAML_R"] = str(R)
+            p2 = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
+                             PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
+                             args.dim, iterations=args.ml_iterations)
+            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            torch.cuda.synchronize(dev)
+            log(rank, f"sweep R={R}: {1e3 * (time.perf_counter() - t0):.1f} ms per call")
+            p2.close()
+        os.environ.pop("GE_FAML_R")
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 #include <vector>
 
@@ -299,78 +300,160 @@ faml_resident(const int* __restrict__ order, const int* __restrict__ pack_beg,
 }
 
 // ---------------------------------------------------------------------------
-// Streamed path for huge aggregates.  Block b covers members
-// [blk_li[b], blk_li[b]+256) of aggregate blk_agg[b].
+// Streamed path for aggregates too large to stay resident.  Per iteration:
+//   faml_big_repulse  the in-aggregate all-pairs sum, one WAVE per work item
+//                     (aggregate a, rows r0 .. r0 + 64R); items are taken from
+//                     an atomic queue in descending-work order (list scheduling
+//                     over aggregates of very different sizes);
+//   faml_big_edges    one wave per member: the CSR row's terms computed 64 at
+//                     a time, added to the repulsion sum in stored order, then
+//                     gravity and the swing/speed update.
+// `rows` lists the P_T positions of all streamed members.
 
-constexpr int kHT = 256;
+constexpr int kHT = 256;   // threads per block of the streamed kernels
+constexpr int kBigW = 64;  // records per wave tile
 
 template <int D>
 __global__ void __launch_bounds__(kHT)
-faml_huge_init(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
-               const int* __restrict__ pt_ip, const int* __restrict__ pt_ix,
+faml_huge_init(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ix,
                const int* __restrict__ vA, const int* __restrict__ ip,
                const int* __restrict__ ix, const double* __restrict__ dx,
                const double* __restrict__ init, double* __restrict__ Xp,
                double* __restrict__ DP, double* __restrict__ Fprev, int use_weights) {
-  const int a = blk_agg[blockIdx.x];
-  const int li = blk_li[blockIdx.x] + threadIdx.x;
-  const int s = pt_ip[a + 1] - pt_ip[a];
-  if (li >= s) return;
-  const int c = pt_ip[a] + li;
+  const int q = blockIdx.x * kHT + threadIdx.x;
+  if (q >= nrows) return;
+  const int c = rows[q];
+  const int v = pt_ix[c];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     Xp[(size_t)c * D + k] = init[(size_t)c * D + k];
     Fprev[(size_t)c * D + k] = 0.0;
   }
-  DP[c] = internal_dp1(pt_ix[c], a, ip, ix, dx, vA, use_weights);
+  DP[c] = internal_dp1(v, vA[v], ip, ix, dx, vA, use_weights);
 }
 
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int D, int R>
+__global__ void __launch_bounds__(kHT)
+faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ queue,
+                 const int* __restrict__ pt_ip, const double* __restrict__ Xp,
+                 const double* __restrict__ DP, double repel, double* __restrict__ Fscr) {
+  constexpr int WV = W<D>::v;
+  __shared__ __attribute__((aligned(16))) double tiles[kHT / 64][kBigW * WV];
+  const int lane = threadIdx.x & 63;
+  double* tile = tiles[threadIdx.x >> 6];
+  const bool repel_ok = weight_ok(repel);
+  for (;;) {
+    int q = 0;
+    if (lane == 0) q = atomicAdd(queue, 1);
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (q >= nitems) break;  // every wave leaves once the queue is drained
+    const int2 item = items[q];
+    const int base = pt_ip[item.x];
+    const int s = pt_ip[item.x + 1] - base;
+    const int r0 = item.y;
+    const int nr = min(R, (s - r0 + 63) >> 6);  // wave-uniform
+    double xi[R][D], di[R], acc[R][D];
+    bool rows_ok = repel_ok;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int li = r0 + lane + 64 * r;
+      const bool ok = r < nr && li < s;
+      const size_t c = (size_t)base + (ok ? li : 0);
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        xi[r][k] = ok ? Xp[c * D + k] : 0.0;
+        acc[r][k] = 0.0;
+      }
+      di[r] = ok ? DP[c] : 1.0;
+      rows_ok = rows_ok && vertex_ok<D>(xi[r], di[r]);
+    }
+    for (int j0 = 0; j0 < s; j0 += kBigW) {
+      const int cnt = min(kBigW, s - j0);
+      bool ok = rows_ok;
+      wave_sync_lds();  // the previous tile has been read by every lane
+      if (lane < cnt) {
+        const size_t c = (size_t)base + j0 + lane;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const double v = Xp[c * D + k];
+          tile[lane * WV + k] = v;
+          ok = ok && coord_ok(v);
+        }
+        const double w = DP[c];
+        tile[lane * WV + D] = w;
+        ok = ok && weight_ok(w);
+      }
+      wave_sync_lds();
+      if (__all(ok)) {
+        for (int jj = 0; jj < cnt; ++jj) {
+          const double* xj = &tile[jj * WV];
+          const double dj = tile[jj * WV + D];
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (r < nr) rep_pair<D, true, false>(xi[r], xj, di[r], dj, repel, acc[r]);
+        }
+      } else {
+        for (int jj = 0; jj < cnt; ++jj) {
+          const double* xj = &tile[jj * WV];
+          const double dj = tile[jj * WV + D];
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (r < nr) rep_pair<D, false, false>(xi[r], xj, di[r], dj, repel, acc[r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int li = r0 + lane + 64 * r;
+      if (r < nr && li < s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) Fscr[((size_t)base + li) * D + k] = acc[r][k];
+      }
+    }
+  }
+}
+
+// One wave per streamed member: CSR terms (:415-467) evaluated 64 at a time,
+// then added to the repulsion sum one by one in stored order (every lane runs
+// the same serial chain on broadcast values), gravity (:469-474) and the
+// update (:477-530).
 template <int D>
 __global__ void __launch_bounds__(kHT)
-faml_huge_force(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
-                const int* __restrict__ pt_ip, const int* __restrict__ pt_ix,
-                const int* __restrict__ pos_of, const int* __restrict__ vA,
-                const int* __restrict__ ip, const int* __restrict__ ix,
-                const double* __restrict__ dx, const double* __restrict__ cA,
-                const double* __restrict__ Xp, const double* __restrict__ DP,
-                double* __restrict__ Fscr, MlConst c) {
-  constexpr int WV = W<D>::v;
-  __shared__ __attribute__((aligned(16))) double tile[kHT * WV];
-  const int a = blk_agg[blockIdx.x];
-  const int base = pt_ip[a];
-  const int s = pt_ip[a + 1] - base;
-  const int li = blk_li[blockIdx.x] + threadIdx.x;
-  const bool ok = li < s;
-  const int cpos = base + (ok ? li : 0);
+faml_big_edges(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ip,
+               const int* __restrict__ pt_ix, const int* __restrict__ pos_of,
+               const int* __restrict__ vA, const int* __restrict__ ip,
+               const int* __restrict__ ix, const double* __restrict__ dx,
+               const double* __restrict__ cA, const double* __restrict__ Xc,
+               double* __restrict__ Xn, const double* __restrict__ DP,
+               const double* __restrict__ Fscr, double* __restrict__ Fprev, MlConst c) {
+  const int w = (blockIdx.x * kHT + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= nrows) return;  // wave-uniform
+  const int cpos = rows[w];
+  const int v = pt_ix[cpos];
+  const int a = vA[v];
+  const int li = cpos - pt_ip[a];
   double xi[D], acc[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    xi[k] = Xp[(size_t)cpos * D + k];
-    acc[k] = 0.0;
+    xi[k] = Xc[(size_t)cpos * D + k];
+    acc[k] = Fscr[(size_t)cpos * D + k];
   }
   const double dip1 = DP[cpos];
   const bool row_ok = all_coord_ok<D>(xi);
-  const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
-  for (int j0 = 0; j0 < s; j0 += kHT) {
-    const int cnt = min(kHT, s - j0);
-    __syncthreads();
-    if ((int)threadIdx.x < cnt) {
-      const int cj = base + j0 + threadIdx.x;
-#pragma unroll
-      for (int k = 0; k < D; ++k) tile[threadIdx.x * WV + k] = Xp[(size_t)cj * D + k];
-      tile[threadIdx.x * WV + D] = DP[cj];
-    }
-    __syncthreads();
-    for (int jj = 0; jj < cnt; ++jj) {
-      const double* xj = &tile[jj * WV];
-      if (rep_ok && vertex_ok<D>(xj, tile[jj * WV + D]))
-        rep_pair<D, true, false>(xi, xj, dip1, tile[jj * WV + D], c.repel, acc);
-      else
-        rep_pair<D, false, false>(xi, xj, dip1, tile[jj * WV + D], c.repel, acc);
-    }
-  }
-  if (!ok) return;
-  // the rest of member_force with the repulsion sum already in acc
   double m2 = xi[0] * xi[0];
 #pragma unroll
   for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
@@ -379,53 +462,52 @@ faml_huge_force(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
   const Recip rmag = recip_of(mag);
   const double* ca = cA + (size_t)a * D;
   const bool ca_ok = all_coord_ok<D>(ca);
-  const int v = pt_ix[cpos];
-  for (int e = ip[v]; e < ip[v + 1]; ++e) {
-    const int j = ix[e];
-    const int b = vA[j];
-    if (b == a && j != li) {
-      const double* xj = Xp + (size_t)pos_of[j] * D;
-      const double w = c.use_weights ? dx[e] : 1.0;
-      if (row_ok && all_coord_ok<D>(xj))
-        attr_edge<D, true>(xi, xj, w, dip1, c, acc);
-      else
-        attr_edge<D, false>(xi, xj, w, dip1, c, acc);
-    } else {
-      const double* cb = cA + (size_t)b * D;
-      if (row_ok && ca_ok && all_coord_ok<D>(cb))
-        pull_edge<D, true>(ca, cb, mag, rmag, acc);
-      else
-        pull_edge<D, false>(ca, cb, mag, rmag, acc);
+  const int e1 = ip[v + 1];
+  for (int e0 = ip[v]; e0 < e1; e0 += 64) {
+    // a term alone: 0 + t == t up to the sign of zero, and acc is never -0
+    // (it starts at +0), so adding it later gives the reference's bits
+    double t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) t[k] = 0.0;
+    const int e = e0 + lane;
+    if (e < e1) {
+      const int j = ix[e];
+      const int b = vA[j];
+      if (b == a && j != li) {  // sic: global j against local i (:417)
+        const double* xj = Xc + (size_t)pos_of[j] * D;
+        const double wt = c.use_weights ? dx[e] : 1.0;
+        if (row_ok && all_coord_ok<D>(xj))
+          attr_edge<D, true>(xi, xj, wt, dip1, c, t);
+        else
+          attr_edge<D, false>(xi, xj, wt, dip1, c, t);
+      } else {
+        const double* cb = cA + (size_t)b * D;
+        if (row_ok && ca_ok && all_coord_ok<D>(cb))
+          pull_edge<D, true>(ca, cb, mag, rmag, t);
+        else
+          pull_edge<D, false>(ca, cb, mag, rmag, t);
+      }
     }
+    const int cnt = min(64, e1 - e0);
+    for (int l = 0; l < cnt; ++l)
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc[k] = acc[k] + lane_bcast(t[k], l);
   }
-  double unit[D];
+  double unit[D], F[D], Fp[D], x[D];
   neg_over<D>(xi, mag, unit);
 #pragma unroll
-  for (int k = 0; k < D; ++k) Fscr[(size_t)cpos * D + k] = acc[k] + unit[k] * c.gravity * dip1;
-}
-
-template <int D>
-__global__ void __launch_bounds__(kHT)
-faml_huge_update(const int* __restrict__ blk_agg, const int* __restrict__ blk_li,
-                 const int* __restrict__ pt_ip, const double* __restrict__ Xc,
-                 double* __restrict__ Xn, const double* __restrict__ Fscr,
-                 double* __restrict__ Fprev, MlConst c) {
-  const int a = blk_agg[blockIdx.x];
-  const int li = blk_li[blockIdx.x] + threadIdx.x;
-  if (li >= pt_ip[a + 1] - pt_ip[a]) return;
-  const size_t cpos = (size_t)(pt_ip[a] + li);
-  double x[D], F[D], Fp[D];
-#pragma unroll
   for (int k = 0; k < D; ++k) {
-    x[k] = Xc[cpos * D + k];
-    F[k] = Fscr[cpos * D + k];
-    Fp[k] = Fprev[cpos * D + k];
+    F[k] = acc[k] + unit[k] * c.gravity * dip1;
+    Fp[k] = Fprev[(size_t)cpos * D + k];
+    x[k] = xi[k];
   }
   member_update<D>(x, F, Fp, c);
+  if (lane == 0) {
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    Xn[cpos * D + k] = x[k];
-    Fprev[cpos * D + k] = F[k];
+    for (int k = 0; k < D; ++k) {
+      Xn[(size_t)cpos * D + k] = x[k];
+      Fprev[(size_t)cpos * D + k] = F[k];
+    }
   }
 }
 
@@ -505,6 +587,38 @@ void build_packs(const std::vector<int>& ids, const int* h_pt_ip, int cap, int m
   if (cnt > 0) beg.push_back((int)order.size());
 }
 
+template <int D>
+void launch_big_repulse(int R, int blocks, hipStream_t st, int nitems, const int2* items,
+                        int* queue, const int* pt_ip, const double* X, const double* DP,
+                        double repel, double* F) {
+  switch (R) {
+    case 4:
+      hipLaunchKernelGGL((faml_big_repulse<D, 4>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
+                         queue, pt_ip, X, DP, repel, F);
+      break;
+    case 2:
+      hipLaunchKernelGGL((faml_big_repulse<D, 2>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
+                         queue, pt_ip, X, DP, repel, F);
+      break;
+    default:
+      hipLaunchKernelGGL((faml_big_repulse<D, 1>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
+                         queue, pt_ip, X, DP, repel, F);
+  }
+}
+
+// resident blocks per CU of faml_big_repulse<dim, R>
+int rep_occupancy(int dim, int R) {
+  int nb = 1;
+  dispatch_dim(dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    const void* k = R == 4   ? (const void*)faml_big_repulse<D, 4>
+                    : R == 2 ? (const void*)faml_big_repulse<D, 2>
+                             : (const void*)faml_big_repulse<D, 1>;
+    GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kHT, 0));
+  });
+  return std::max(nb, 1);
+}
+
 }  // namespace
 
 }  // namespace ge
@@ -518,9 +632,11 @@ struct ge_faml_plan {
   const int *ip = nullptr, *ix = nullptr, *pt_ip = nullptr, *pt_ix = nullptr, *vA = nullptr;
   const double* dx = nullptr;
   ge::FaConst c{};
-  int ns = 0, nm = 0, nl = 0, nb = 0, nhuge = 0;
+  int ns = 0, nm = 0, nl = 0, nhuge = 0;
   size_t off_m = 0, off_l = 0;
-  ge::DevBuf<int> pos, order, beg, blk_agg, blk_li, huge;
+  ge::DevBuf<int> pos, order, beg, rows, queue, huge;
+  ge::DevBuf<int2> items;
+  int nrows = 0, nitems = 0, R = 1, rep_blocks = 0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
   // the size classes are independent: streamed path, large, mid and small
   // packs each run on their own stream and join the context stream at the end
@@ -574,12 +690,34 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
   build_packs(small, h_pt_ip, 64, 64, order, beg_s);
   build_packs(mid, h_pt_ip, 256, 256, order, beg_m);
   build_packs(large, h_pt_ip, large_cap(dim), 1, order, beg_l);
-  std::vector<int> blk_agg, blk_li;
+  // streamed members and their repulsion work items (aggregate, first row):
+  // R row slots of 64 per wave, taken in descending-work order
+  std::vector<int> rows;
   for (int a : big)
-    for (int li = 0; li < h_pt_ip[a + 1] - h_pt_ip[a]; li += kHT) {
-      blk_agg.push_back(a);
-      blk_li.push_back(li);
+    for (int li = 0; li < h_pt_ip[a + 1] - h_pt_ip[a]; ++li) rows.push_back(h_pt_ip[a] + li);
+  int R = 0;
+  if (const char* e = std::getenv("GE_FAML_R")) R = std::atoi(e);
+  if (R != 1 && R != 2 && R != 4) {
+    // enough items for ~2 per wave slot at the occupancy of the R variant
+    R = 1;
+    for (int r : {4, 2}) {
+      const double slots = (double)cus * rep_occupancy(dim, r) * (kHT / 64);
+      if ((double)rows.size() / (64.0 * r) >= 2.0 * slots) { R = r; break; }
     }
+  }
+  struct Item { int a, r0; double work; };
+  std::vector<Item> its;
+  for (int a : big) {
+    const int s = h_pt_ip[a + 1] - h_pt_ip[a];
+    for (int r0 = 0; r0 < s; r0 += 64 * R)
+      its.push_back({a, r0, (double)std::min(R, (s - r0 + 63) / 64) * s});
+  }
+  std::stable_sort(its.begin(), its.end(),
+                   [](const Item& x, const Item& y) { return x.work > y.work; });
+  std::vector<int2> items;
+  for (const Item& it : its) items.push_back(make_int2(it.a, it.r0));
+  pl->R = R;
+  pl->rep_blocks = cus * rep_occupancy(dim, R);
   std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
   pl->off_m = begs.size();
@@ -589,24 +727,26 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
   pl->ns = (int)beg_s.size() - 1;
   pl->nm = (int)beg_m.size() - 1;
   pl->nl = (int)beg_l.size() - 1;
-  pl->nb = (int)blk_agg.size();
+  pl->nrows = (int)rows.size();
+  pl->nitems = (int)items.size();
   pl->nhuge = (int)big.size();
 
   const int n = pl->n;
   pl->pos.alloc(std::max(n, 1));
   pl->order.alloc(std::max<size_t>(order.size(), 1));
   pl->beg.alloc(std::max<size_t>(begs.size(), 1));
-  pl->blk_agg.alloc(std::max<size_t>(blk_agg.size(), 1));
-  pl->blk_li.alloc(std::max<size_t>(blk_li.size(), 1));
+  pl->rows.alloc(std::max<size_t>(rows.size(), 1));
+  pl->items.alloc(std::max<size_t>(items.size(), 1));
+  pl->queue.alloc(std::max(pl->iterations, 1));
   pl->huge.alloc(std::max<size_t>(big.size(), 1));
   pl->order.upload(order.data(), order.size(), st);
   pl->beg.upload(begs.data(), begs.size(), st);
-  pl->blk_agg.upload(blk_agg.data(), blk_agg.size(), st);
-  pl->blk_li.upload(blk_li.data(), blk_li.size(), st);
+  pl->rows.upload(rows.data(), rows.size(), st);
+  pl->items.upload(items.data(), items.size(), st);
   pl->huge.upload(big.data(), big.size(), st);
   pl->Fscr.alloc((size_t)std::max(n, 1) * dim);
   pl->Fprev.alloc((size_t)std::max(n, 1) * dim);
-  if (pl->nb > 0) {
+  if (pl->nrows > 0) {
     pl->Xa.alloc((size_t)n * dim);
     pl->Xb.alloc((size_t)n * dim);
     pl->DP.alloc(n);
@@ -646,18 +786,21 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     // streamed path (side[0])
     hipStream_t ss = pl->side[0];
     if (ev) GE_HIP(hipEventRecord(ev[2], ss));
-    if (pl->nb > 0) {
-      hipLaunchKernelGGL((faml_huge_init<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
-                         pl->blk_li.p, pl->pt_ip, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, init,
+    if (pl->nrows > 0) {
+      const int nr = pl->nrows;
+      hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
+                         nr, pl->rows.p, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, init,
                          pl->Xa.p, pl->DP.p, pl->Fprev.p, c.use_weights);
+      GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
-        hipLaunchKernelGGL((faml_huge_force<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
-                           pl->blk_li.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
-                           pl->dx, cA, cur, pl->DP.p, pl->Fscr.p, c);
-        hipLaunchKernelGGL((faml_huge_update<D>), dim3(pl->nb), dim3(kHT), 0, ss, pl->blk_agg.p,
-                           pl->blk_li.p, pl->pt_ip, cur, nxt, pl->Fscr.p, pl->Fprev.p, c);
+        launch_big_repulse<D>(pl->R, pl->rep_blocks, ss, pl->nitems, pl->items.p,
+                              pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
+        hipLaunchKernelGGL((faml_big_edges<D>), dim3((nr + kHT / 64 - 1) / (kHT / 64)),
+                           dim3(kHT), 0, ss, nr, pl->rows.p, pl->pt_ip, pl->pt_ix, pl->pos.p,
+                           pl->vA, pl->ip, pl->ix, pl->dx, cA, cur, nxt, pl->DP.p, pl->Fscr.p,
+                           pl->Fprev.p, c);
         std::swap(cur, nxt);
       }
       hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,

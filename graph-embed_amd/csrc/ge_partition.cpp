@@ -68,6 +68,14 @@ class NbrMap {
     }
     place(at, k, 0.0 + v);
   }
+  const double* find(int k) const {
+    if (keys_.empty()) return nullptr;
+    const int mask = (int)keys_.size() - 1;
+    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
+      if (keys_[h] == k) return &vals_[h];
+      if (keys_[h] == kEmpty) return nullptr;
+    }
+  }
   void erase(int k) {
     if (keys_.empty()) return;
     const int mask = (int)keys_.size() - 1;
@@ -79,6 +87,13 @@ class NbrMap {
       }
       if (keys_[h] == kEmpty) return;
     }
+  }
+  int capacity() const { return (int)keys_.size(); }
+  // visit slots [b, e) (for splitting one large map across threads)
+  template <class F>
+  void for_range(int b, int e, F&& f) const {
+    for (int h = b; h < e; ++h)
+      if (keys_[h] >= 0) f(keys_[h], vals_[h]);
   }
   template <class F>
   void for_each(F&& f) const {
@@ -191,15 +206,23 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   std::vector<char> dead(n, 0), busy(n, 0), dirty(n, 1);
   std::vector<double> best(n, -inf);
   std::vector<int> arg(n, 0);
+  // runner-up of each clean vertex's last scan (value, index) under the same
+  // order (eta descending, index ascending).  Etas only fall while a vertex stays
+  // clean, so it is an upper bound on the current runner-up.
+  std::vector<double> second(n, -inf);
+  std::vector<int> second_idx(n, -1);
   std::vector<int> work(n);  // dirty vertices
   std::iota(work.begin(), work.end(), 0);
   Bitmap cand;  // over `alive` slots: max_ind != -1 (and max_eta > 0 if positive)
   cand.resize(n);
 
+  long long msrc[6] = {0, 0, 0, 0, 0, 0};
+  int mcur = 0;
   auto mark = [&](int v) {
     if (!dirty[v]) {
       dirty[v] = 1;
       work.push_back(v);
+      ++msrc[mcur];
     }
   };
   auto mark_nbrs = [&](int v) { adj[v].for_each([&](int k, double) { mark(k); }); };
@@ -208,6 +231,59 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     if (c) cand.set(slot[v]);
     else cand.clr(slot[v]);
   };
+  // watch[v]: clean vertices whose max_ind is v (entries may be stale; checked
+  // on use).  Invariant: every clean k with arg[k] = v >= 0 is in watch[v].
+  std::vector<std::vector<int>> watch(n);
+  auto consume = [&](int v) {
+    for (int k : watch[v])
+      if (arg[k] == v) mark(k);
+    std::vector<int>().swap(watch[v]);
+  };
+  // v became busy: a clean watcher k whose only candidate was v (no runner-up)
+  // now has none -- exactly what its rescan would find -- and gets v back at
+  // the end of the round if v survives; the others rescan.
+  std::vector<std::pair<int, int>> lost;
+  auto consume_busy = [&](int v) {
+    for (int k : watch[v]) {
+      if (arg[k] != v || dirty[k]) continue;
+      if (second_idx[k] < 0) {
+        best[k] = -inf;
+        arg[k] = -1;
+        set_cand(k);
+        lost.emplace_back(k, v);
+      } else {
+        mark(k);
+      }
+    }
+    std::vector<int>().swap(watch[v]);
+  };
+  // keep's alpha grew: a clean watcher k keeps keep as its max if the new eta
+  // still beats the (upper bound of the) runner-up; then only max_eta changes.
+  std::vector<int> stay;
+  auto reeval = [&](int v) {
+    stay.clear();
+    for (int k : watch[v]) {
+      if (arg[k] != v || dirty[k]) continue;
+      const double* w = adj[k].find(v);
+      bool kept = false;
+      if (w) {
+        const double eta = 2 * (*w / T - alpha[k] * alpha[v]);
+        if (second_idx[k] < 0 || eta > second[k] || (eta == second[k] && v < second_idx[k])) {
+          best[k] = eta;
+          set_cand(k);
+          stay.push_back(k);
+          kept = true;
+        }
+      }
+      if (!kept) mark(k);
+    }
+    watch[v].swap(stay);
+  };
+  // With positive weights every alpha is positive, so a merge only lowers the
+  // eta of keep's neighbours towards keep: only vertices whose max_ind is keep
+  // (watchers) can change, plus anything scanned while keep was busy.
+  bool positive_weights = true;
+  for (long long e = 0; e < (long long)I[n]; ++e) positive_weights = positive_weights && Dv[e] > 0;
   auto root = [&](int x) {
     int r = x;
     while (up[r] != r) r = up[r];
@@ -234,10 +310,10 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     h->indices.push_back(std::move(ix));
   };
 
-  double t_scan = 0, t_resolve = 0, t_merge = 0, t_pop = 0;
+  double t_scan = 0, t_resolve = 0, t_merge = 0, t_pop = 0, t_cls = 0, t_par = 0;
   long long rescans = 0;
   int rounds = 0;
-  std::vector<int> todo, keep_dirty;
+  std::vector<int> todo, keep_dirty, late, big, small_todo;
   int M_prev = M;
   do {
     ++rounds;
@@ -259,26 +335,76 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
         }
       }
       work.swap(keep_dirty);
+      const auto tA = now();
+      t_cls += secs(t0, tA);
       const int nt = (int)todo.size();
       rescans += nt;
+      // top-2 under (eta descending, index ascending): a total order, so any
+      // split of a neighbourhood reduces to the same result
+      struct Top2 {
+        double e1 = -std::numeric_limits<double>::infinity(), e2 = e1;
+        int i1 = -1, i2 = -1;
+        void offer(double e, int j) {
+          if (i1 < 0 || e > e1 || (e == e1 && j < i1)) {
+            e2 = e1;
+            i2 = i1;
+            e1 = e;
+            i1 = j;
+          } else if (i2 < 0 || e > e2 || (e == e2 && j < i2)) {
+            e2 = e;
+            i2 = j;
+          }
+        }
+      };
+      auto scan_range = [&](int i, int b, int e, Top2& t) {
+        const double ai = alpha[i];
+        adj[i].for_range(b, e, [&](int j, double w) {
+          if (busy[j]) return;
+          t.offer(2 * (w / T - ai * alpha[j]), j);
+        });
+      };
+      auto store = [&](int i, const Top2& t) {
+        best[i] = t.e1;
+        arg[i] = t.i1;
+        second[i] = t.e2;
+        second_idx[i] = t.i2;
+      };
+      big.clear();
+      small_todo.clear();
+      for (int x = 0; x < nt; ++x)
+        (adj[todo[x]].capacity() > 8192 ? big : small_todo).push_back(todo[x]);
+      const int nsm = (int)small_todo.size();
 #pragma omp parallel for schedule(dynamic, 64)
+      for (int x = 0; x < nsm; ++x) {
+        Top2 t;
+        const int i = small_todo[x];
+        scan_range(i, 0, adj[i].capacity(), t);
+        store(i, t);
+      }
+      for (int i : big) {  // one large neighbourhood split across threads
+        const int cap = adj[i].capacity();
+        Top2 acc;
+#pragma omp parallel
+        {
+          Top2 t;
+#pragma omp for schedule(static) nowait
+          for (int b = 0; b < cap; b += 1024) scan_range(i, b, std::min(cap, b + 1024), t);
+#pragma omp critical
+          {
+            if (t.i1 >= 0) acc.offer(t.e1, t.i1);
+            if (t.i2 >= 0) acc.offer(t.e2, t.i2);
+          }
+        }
+        store(i, acc);
+      }
+      const auto tB = now();
+      t_par += secs(tA, tB);
       for (int x = 0; x < nt; ++x) {
         const int i = todo[x];
-        double top = -inf;
-        int who = -1;
-        const double ai = alpha[i];
-        adj[i].for_each([&](int j, double w) {
-          if (busy[j]) return;
-          const double eta = 2 * (w / T - ai * alpha[j]);
-          if (eta > top || (eta == top && j < who)) {
-            top = eta;
-            who = j;
-          }
-        });
-        best[i] = top;
-        arg[i] = who;
+        set_cand(i);
+        if (arg[i] >= 0) watch[arg[i]].push_back(i);
+        if (pass > 0) late.push_back(i);  // scanned while this round's pairs were busy
       }
-      for (int x = 0; x < nt; ++x) set_cand(todo[x]);
       const auto t1 = now();
       t_scan += secs(t0, t1);
       // ---- greedy resolve in `used` order (:1728-1753)
@@ -299,8 +425,14 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
           else
             merges.emplace_back(i, j);
           busy[i] = busy[j] = 1;
-          mark_nbrs(i);  // their candidate sets lost i and j
-          mark_nbrs(j);
+          mcur = 1;
+          if (positive_weights) {  // only vertices whose max_ind is i or j lose their max
+            consume_busy(i);
+            consume_busy(j);
+          } else {
+            mark_nbrs(i);
+            mark_nbrs(j);
+          }
           dQ += best[i];
         }
       }
@@ -310,6 +442,7 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     const auto t2 = now();
     for (const auto& mg : merges) {
       const int keep = mg.first, gone = mg.second;
+      mcur = 2;
       adj[gone].for_each([&](int k, double w) {
         adj[k].erase(gone);
         best[k] = -inf;
@@ -324,8 +457,19 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       });
       adj[gone].clear();
       mark(keep);
-      mark_nbrs(keep);  // alpha[keep] changed; keep becomes a candidate again
+      mcur = 3;
+      if (positive_weights) {
+        reeval(keep);  // eta towards keep fell for everyone; only its watchers can change
+        consume(gone);
+      } else {
+        mark_nbrs(keep);
+      }
     }
+    // vertices scanned in passes >= 2 excluded this round's busy pairs; the
+    // surviving ones become available again now
+    mcur = 4;
+    for (int v : late) mark(v);
+    late.clear();
     Q += dQ;
     M_prev = M;
     const auto t3 = now();
@@ -353,6 +497,23 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       busy[keep] = 0;
       M -= 1;
     }
+    // single-candidate vertices that lost their partner to busy get it back
+    // (it was scanned in pass 1, when nothing was busy, so v is its only
+    // neighbour; any change to its adjacency would have marked it dirty)
+    for (const auto& kv : lost) {
+      const int k = kv.first, v = kv.second;
+      if (dirty[k] || dead[k] || arg[k] != -1) continue;
+      const double* w = dead[v] ? nullptr : adj[k].find(v);
+      if (!w) {
+        mark(k);
+        continue;
+      }
+      best[k] = 2 * (*w / T - alpha[k] * alpha[v]);
+      arg[k] = v;
+      set_cand(k);
+      watch[v].push_back(k);
+    }
+    lost.clear();
     t_pop += secs(t3, now());
     if (prof && std::getenv("GE_PROFILE_ROUNDS"))
       std::fprintf(stderr, "round %d alive %d merges %zu rescans_total %lld\n", rounds, M,
@@ -364,6 +525,11 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
                  "partition: n=%d %d rounds %.3fs: scan %.3fs (%lld rescans) resolve %.3fs "
                  "merge %.3fs snap+pop %.3fs\n",
                  n, rounds, secs(t_start, now()), t_scan, rescans, t_resolve, t_merge, t_pop);
+  if (prof)
+    std::fprintf(stderr, "scan split: classify %.3fs parallel %.3fs\n", t_cls, t_par);
+  if (prof)
+    std::fprintf(stderr, "marks: init %lld resolve %lld gone-nbrs %lld keep %lld late %lld\n",
+                 msrc[0], msrc[1], msrc[2], msrc[3], msrc[4]);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;
     std::cout << "level 0: " << n << " aggregates" << std::endl;

@@ -169,6 +169,25 @@ def test_faml_size_classes(ctx, oracle, sizes):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("R", [1, 2, 4])
+def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R):
+    """Streamed path (faml_big_repulse / faml_big_edges) with 1, 2 and 4 row
+    slots per lane, ragged last items, and hub rows longer than one 64-edge chunk."""
+    monkeypatch.setenv("GE_FAML_R", str(R))
+    sizes = [3000, 700, 2203, 90, 1]
+    n = sum(sizes)
+    A = G.submatrix(G.rmat(n, 10 * n, seed=7), np.arange(n))
+    assert np.diff(A[0]).max() > 128
+    PT = _block_partition(n, sizes, seed=3)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, 3, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("dim", [2, 4])
 def test_faml_dims(ctx, oracle, dim):
     A = G.largest_component(G.rmat(1500, 9000, seed=dim))
