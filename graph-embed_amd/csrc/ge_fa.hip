@@ -38,6 +38,7 @@
 
 #include "ge_internal.hpp"
 #include "ge_pair.hpp"
+#include "ge_rows.hpp"
 
 namespace ge {
 namespace {
@@ -251,13 +252,13 @@ __global__ void fa_reduce_parts(int rows, int jblocks, const double* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Attraction + gravity + swing + update, one thread per row (serial CSR order).
+// Attraction + gravity + swing + update per row (serial CSR order).
 
 template <int D>
 __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D], double (&acc)[D],
                                            double dip1, const FaConst& c,
                                            double* __restrict__ Fprev,
-                                           double* __restrict__ Xnext) {
+                                           double* __restrict__ Xnext, bool write = true) {
   double m2 = xi[0] * xi[0];
 #pragma unroll
   for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
@@ -281,6 +282,7 @@ __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D],
   double speed = c.ks_gS / (1 + c.gS * sqrt(swing));
   const double cap = c.ksmax / totalF;
   if (speed > cap) speed = cap;
+  if (!write) return;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     Xnext[(size_t)i * D + k] = F[k] * speed + xi[k];
@@ -288,34 +290,44 @@ __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D],
   }
 }
 
+// Row policy for classed_rows_kernel (ge_rows.hpp): attraction (:169-203) added
+// to the repulsion sum in CSR order, then gravity, swing and update.
 template <int D>
-__global__ void __launch_bounds__(256)
-fa_attract_update_strict(int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
-                         const double* __restrict__ dx, const double* __restrict__ X,
-                         const double* __restrict__ dp1, const double* __restrict__ Frep,
-                         double* __restrict__ Fprev, double* __restrict__ Xnext, FaConst c) {
-  const int i = rb + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= re) return;
-  const int li = i - rb;
-  double xi[D], acc[D];
+struct FaRows {
+  int rb;
+  const int *ip, *ix;
+  const double *dx, *X, *dp1, *Frep;
+  double *Fprev, *Xnext;
+  FaConst c;
+  struct State {
+    int i, e0, e1;
+    double xi[D], acc[D], dip1;
+    bool row_ok;
+  };
+  __device__ __forceinline__ void load(int i, State& s) const {
+    s.i = i;
+    s.e0 = ip[i];
+    s.e1 = ip[i + 1];
 #pragma unroll
-  for (int k = 0; k < D; ++k) {
-    xi[k] = X[(size_t)i * D + k];
-    acc[k] = Frep[(size_t)li * D + k];
+    for (int k = 0; k < D; ++k) {
+      s.xi[k] = X[(size_t)i * D + k];
+      s.acc[k] = Frep[(size_t)(i - rb) * D + k];
+    }
+    s.dip1 = dp1[i];
+    s.row_ok = all_coord_ok<D>(s.xi);
   }
-  const bool row_ok = all_coord_ok<D>(xi);
-  const double dip1 = dp1[i];
-  const int e1 = ip[i + 1];
-  for (int e = ip[i]; e < e1; ++e) {
+  __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
     const double* xj = X + (size_t)ix[e] * D;
     const double a = c.use_weights ? dx[e] : 1.0;
-    if (row_ok && all_coord_ok<D>(xj))
-      attr_edge<D, true>(xi, xj, a, dip1, c, acc);
+    if (s.row_ok && all_coord_ok<D>(xj))
+      attr_edge<D, true>(s.xi, xj, a, s.dip1, c, t);
     else
-      attr_edge<D, false>(xi, xj, a, dip1, c, acc);
+      attr_edge<D, false>(s.xi, xj, a, s.dip1, c, t);
   }
-  finish_row<D>(i, li, xi, acc, dip1, c, Fprev, Xnext);
-}
+  __device__ __forceinline__ void finish(State& s, bool writer) const {
+    finish_row<D>(s.i, s.i - rb, s.xi, s.acc, s.dip1, c, Fprev, Xnext, writer);
+  }
+};
 
 // ---------------------------------------------------------------------------
 // Small graphs: one workgroup runs every iteration, coordinates in LDS.
@@ -453,13 +465,13 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
 }
 
 template <int D>
-void launch_attract(hipStream_t s, int rb, int re, const int* ip, const int* ix,
+void launch_attract(hipStream_t s, const RowClasses& rc, int rb, const int* ip, const int* ix,
                     const double* dx, const double* X, const double* dp1, const double* Frep,
                     double* Fprev, double* Xnext, const FaConst& c) {
-  const int rows = re - rb;
-  if (rows <= 0) return;
-  hipLaunchKernelGGL((fa_attract_update_strict<D>), dim3((rows + 255) / 256), dim3(256), 0, s,
-                     rb, re, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c);
+  if (rc.grid() == 0) return;
+  const FaRows<D> fr{rb, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c};
+  hipLaunchKernelGGL((classed_rows_kernel<D, FaRows<D>>), dim3(rc.grid()), dim3(kRowT), 0, s, rc,
+                     fr);
 }
 
 }  // namespace
@@ -477,6 +489,8 @@ struct ge_fa_plan {
   ge_fa_params p{};
   ge::FaConst c{};
   ge::DevBuf<double> dp1, frep, fprev, fpart;
+  ge::DevBuf<int> rows;  // rb..re in degree classes (ge_rows.hpp)
+  ge::RowClasses rc;
   int cus = 256;
   bool profiling = false;
   std::vector<hipEvent_t> events;  // 3 per timed step
@@ -494,6 +508,21 @@ static void plan_init(ge_fa_plan* pl) {
   if (pl->p.mode == GE_MODE_FAST)
     pl->fpart.alloc((size_t)std::max(rows, 1) * pl->dim * kFastJBlocks);
   hipStream_t s = pl->ctx->stream;
+  if (rows > 0) {
+    std::vector<int> h_ip(pl->re - pl->rb + 1), ids(rows), deg(rows), order;
+    GE_HIP(hipMemcpyAsync(h_ip.data(), pl->ip + pl->rb, sizeof(int) * h_ip.size(),
+                          hipMemcpyDeviceToHost, s));
+    GE_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < rows; ++q) {
+      ids[q] = pl->rb + q;
+      deg[q] = h_ip[q + 1] - h_ip[q];
+    }
+    classify_rows(ids, deg, order, pl->rc.nheavy, pl->rc.nmed, pl->rc.nlight);
+    pl->rows.alloc(rows);
+    pl->rows.upload(order.data(), rows, s);
+    pl->rc.rows = pl->rows.p;
+    GE_HIP(hipStreamSynchronize(s));
+  }
   hipLaunchKernelGGL(degp1_kernel, dim3((pl->n + 255) / 256), dim3(256), 0, s, pl->n, pl->ip,
                      pl->dx, pl->p.use_weights, pl->dp1.p);
   GE_HIP(hipGetLastError());
@@ -520,7 +549,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
     launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
                         pl->frep.p, pl->fpart.p, pl->cus);
     if (ev) GE_HIP(hipEventRecord(ev[1], s));
-    launch_attract<D>(s, pl->rb, pl->re, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
+    launch_attract<D>(s, pl->rc, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
                       pl->fprev.p, xn, pl->c);
   });
   GE_HIP(hipGetLastError());

@@ -35,6 +35,7 @@
 
 #include "ge_internal.hpp"
 #include "ge_pair.hpp"
+#include "ge_rows.hpp"
 
 namespace ge {
 namespace {
@@ -305,9 +306,9 @@ faml_resident(const int* __restrict__ order, const int* __restrict__ pack_beg,
 //                     (aggregate a, rows r0 .. r0 + 64R); items are taken from
 //                     an atomic queue in descending-work order (list scheduling
 //                     over aggregates of very different sizes);
-//   faml_big_edges    one wave per member: the CSR row's terms computed 64 at
-//                     a time, added to the repulsion sum in stored order, then
-//                     gravity and the swing/speed update.
+//   FamlRows          (classed_rows_kernel, ge_rows.hpp) the CSR row's terms
+//                     added to the repulsion sum in stored order, then gravity
+//                     and the swing/speed update.
 // `rows` lists the P_T positions of all streamed members.
 
 constexpr int kHT = 256;   // threads per block of the streamed kernels
@@ -330,19 +331,6 @@ faml_huge_init(int nrows, const int* __restrict__ rows, const int* __restrict__ 
     Fprev[(size_t)c * D + k] = 0.0;
   }
   DP[c] = internal_dp1(v, vA[v], ip, ix, dx, vA, use_weights);
-}
-
-__device__ __forceinline__ double lane_bcast(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-__device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <int D, int R>
@@ -383,7 +371,7 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
     for (int j0 = 0; j0 < s; j0 += kBigW) {
       const int cnt = min(kBigW, s - j0);
       bool ok = rows_ok;
-      wave_sync_lds();  // the previous tile has been read by every lane
+      wave_lds_sync();  // the previous tile has been read by every lane
       if (lane < cnt) {
         const size_t c = (size_t)base + j0 + lane;
 #pragma unroll
@@ -396,7 +384,7 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
         tile[lane * WV + D] = w;
         ok = ok && weight_ok(w);
       }
-      wave_sync_lds();
+      wave_lds_sync();
       if (__all(ok)) {
         for (int jj = 0; jj < cnt; ++jj) {
           const double* xj = &tile[jj * WV];
@@ -426,90 +414,81 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
   }
 }
 
-// One wave per streamed member: CSR terms (:415-467) evaluated 64 at a time,
-// then added to the repulsion sum one by one in stored order (every lane runs
-// the same serial chain on broadcast values), gravity (:469-474) and the
-// update (:477-530).
+// Per streamed member, after faml_big_repulse: the CSR row (:415-467) added to
+// the repulsion sum in stored order (degree-classed, ge_rows.hpp), gravity
+// (:469-474) and the swing/speed update (:477-530).
 template <int D>
-__global__ void __launch_bounds__(kHT)
-faml_big_edges(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ip,
-               const int* __restrict__ pt_ix, const int* __restrict__ pos_of,
-               const int* __restrict__ vA, const int* __restrict__ ip,
-               const int* __restrict__ ix, const double* __restrict__ dx,
-               const double* __restrict__ cA, const double* __restrict__ Xc,
-               double* __restrict__ Xn, const double* __restrict__ DP,
-               const double* __restrict__ Fscr, double* __restrict__ Fprev, MlConst c) {
-  const int w = (blockIdx.x * kHT + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (w >= nrows) return;  // wave-uniform
-  const int cpos = rows[w];
-  const int v = pt_ix[cpos];
-  const int a = vA[v];
-  const int li = cpos - pt_ip[a];
-  double xi[D], acc[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    xi[k] = Xc[(size_t)cpos * D + k];
-    acc[k] = Fscr[(size_t)cpos * D + k];
-  }
-  const double dip1 = DP[cpos];
-  const bool row_ok = all_coord_ok<D>(xi);
-  double m2 = xi[0] * xi[0];
-#pragma unroll
-  for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
-  double mag = sqrt(m2);
-  if (mag < kEps) mag = kEps;
-  const Recip rmag = recip_of(mag);
-  const double* ca = cA + (size_t)a * D;
-  const bool ca_ok = all_coord_ok<D>(ca);
-  const int e1 = ip[v + 1];
-  for (int e0 = ip[v]; e0 < e1; e0 += 64) {
-    // a term alone: 0 + t == t up to the sign of zero, and acc is never -0
-    // (it starts at +0), so adding it later gives the reference's bits
-    double t[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) t[k] = 0.0;
-    const int e = e0 + lane;
-    if (e < e1) {
-      const int j = ix[e];
-      const int b = vA[j];
-      if (b == a && j != li) {  // sic: global j against local i (:417)
-        const double* xj = Xc + (size_t)pos_of[j] * D;
-        const double wt = c.use_weights ? dx[e] : 1.0;
-        if (row_ok && all_coord_ok<D>(xj))
-          attr_edge<D, true>(xi, xj, wt, dip1, c, t);
-        else
-          attr_edge<D, false>(xi, xj, wt, dip1, c, t);
-      } else {
-        const double* cb = cA + (size_t)b * D;
-        if (row_ok && ca_ok && all_coord_ok<D>(cb))
-          pull_edge<D, true>(ca, cb, mag, rmag, t);
-        else
-          pull_edge<D, false>(ca, cb, mag, rmag, t);
-      }
-    }
-    const int cnt = min(64, e1 - e0);
-    for (int l = 0; l < cnt; ++l)
-#pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + lane_bcast(t[k], l);
-  }
-  double unit[D], F[D], Fp[D], x[D];
-  neg_over<D>(xi, mag, unit);
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    F[k] = acc[k] + unit[k] * c.gravity * dip1;
-    Fp[k] = Fprev[(size_t)cpos * D + k];
-    x[k] = xi[k];
-  }
-  member_update<D>(x, F, Fp, c);
-  if (lane == 0) {
+struct FamlRows {
+  const int *pt_ip, *pt_ix, *pos_of, *vA, *ip, *ix;
+  const double *dx, *cA, *Xc, *DP, *Fscr;
+  double *Xn, *Fprev;
+  MlConst c;
+  struct State {
+    int cpos, a, li, e0, e1;
+    double xi[D], acc[D], dip1, mag;
+    Recip rmag;
+    bool row_ok, ca_ok;
+  };
+  __device__ __forceinline__ void load(int cpos, State& s) const {
+    const int v = pt_ix[cpos];
+    s.cpos = cpos;
+    s.a = vA[v];
+    s.li = cpos - pt_ip[s.a];
+    s.e0 = ip[v];
+    s.e1 = ip[v + 1];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      Xn[(size_t)cpos * D + k] = x[k];
-      Fprev[(size_t)cpos * D + k] = F[k];
+      s.xi[k] = Xc[(size_t)cpos * D + k];
+      s.acc[k] = Fscr[(size_t)cpos * D + k];
+    }
+    s.dip1 = DP[cpos];
+    s.row_ok = all_coord_ok<D>(s.xi);
+    double m2 = s.xi[0] * s.xi[0];
+#pragma unroll
+    for (int k = 1; k < D; ++k) m2 = m2 + s.xi[k] * s.xi[k];
+    s.mag = sqrt(m2);
+    if (s.mag < kEps) s.mag = kEps;
+    s.rmag = recip_of(s.mag);
+    s.ca_ok = all_coord_ok<D>(cA + (size_t)s.a * D);
+  }
+  __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
+    const int j = ix[e];
+    const int b = vA[j];
+    if (b == s.a && j != s.li) {  // sic: global j against local i (:417)
+      const double* xj = Xc + (size_t)pos_of[j] * D;
+      const double wt = c.use_weights ? dx[e] : 1.0;
+      if (s.row_ok && all_coord_ok<D>(xj))
+        attr_edge<D, true>(s.xi, xj, wt, s.dip1, c, t);
+      else
+        attr_edge<D, false>(s.xi, xj, wt, s.dip1, c, t);
+    } else {
+      const double* ca = cA + (size_t)s.a * D;
+      const double* cb = cA + (size_t)b * D;
+      if (s.row_ok && s.ca_ok && all_coord_ok<D>(cb))
+        pull_edge<D, true>(ca, cb, s.mag, s.rmag, t);
+      else
+        pull_edge<D, false>(ca, cb, s.mag, s.rmag, t);
     }
   }
-}
+  __device__ __forceinline__ void finish(State& s, bool writer) const {
+    double unit[D], F[D], Fp[D], x[D];
+    neg_over<D>(s.xi, s.mag, unit);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      F[k] = s.acc[k] + unit[k] * c.gravity * s.dip1;
+      Fp[k] = Fprev[(size_t)s.cpos * D + k];
+      x[k] = s.xi[k];
+    }
+    member_update<D>(x, F, Fp, c);
+    if (writer) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        Xn[(size_t)s.cpos * D + k] = x[k];
+        Fprev[(size_t)s.cpos * D + k] = F[k];
+      }
+    }
+  }
+};
 
 // One block per huge aggregate: serial mean by lane 0, max by reduction.
 template <int D>
@@ -634,7 +613,8 @@ struct ge_faml_plan {
   ge::FaConst c{};
   int ns = 0, nm = 0, nl = 0, nhuge = 0;
   size_t off_m = 0, off_l = 0;
-  ge::DevBuf<int> pos, order, beg, rows, queue, huge;
+  ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge;
+  ge::RowClasses ecls;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, rep_blocks = 0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
@@ -704,6 +684,23 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
       const double slots = (double)cus * rep_occupancy(dim, r) * (kHT / 64);
       if ((double)rows.size() / (64.0 * r) >= 2.0 * slots) { R = r; break; }
     }
+  }
+  std::vector<int> erows;
+  if (!rows.empty()) {  // degree classes of the streamed members' CSR rows
+    std::vector<int> h_ip(pl->n + 1), h_ptix(pl->n);
+    GE_HIP(hipMemcpyAsync(h_ip.data(), pl->ip, sizeof(int) * (pl->n + 1), hipMemcpyDeviceToHost, st));
+    GE_HIP(hipMemcpyAsync(h_ptix.data(), pl->pt_ix, sizeof(int) * pl->n, hipMemcpyDeviceToHost,
+                          st));
+    GE_HIP(hipStreamSynchronize(st));
+    std::vector<int> deg(rows.size());
+    for (size_t q = 0; q < rows.size(); ++q) {
+      const int v = h_ptix[rows[q]];
+      deg[q] = h_ip[v + 1] - h_ip[v];
+    }
+    classify_rows(rows, deg, erows, pl->ecls.nheavy, pl->ecls.nmed, pl->ecls.nlight);
+    pl->erows.alloc(erows.size());
+    pl->erows.upload(erows.data(), erows.size(), st);
+    pl->ecls.rows = pl->erows.p;
   }
   struct Item { int a, r0; double work; };
   std::vector<Item> its;
@@ -797,10 +794,10 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       for (int it = 0; it < iters; ++it) {
         launch_big_repulse<D>(pl->R, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                               pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
-        hipLaunchKernelGGL((faml_big_edges<D>), dim3((nr + kHT / 64 - 1) / (kHT / 64)),
-                           dim3(kHT), 0, ss, nr, pl->rows.p, pl->pt_ip, pl->pt_ix, pl->pos.p,
-                           pl->vA, pl->ip, pl->ix, pl->dx, cA, cur, nxt, pl->DP.p, pl->Fscr.p,
-                           pl->Fprev.p, c);
+        const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx,
+                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
+        hipLaunchKernelGGL((classed_rows_kernel<D, FamlRows<D>>), dim3(pl->ecls.grid()),
+                           dim3(kRowT), 0, ss, pl->ecls, fr);
         std::swap(cur, nxt);
       }
       hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,

@@ -1,0 +1,138 @@
+// ge_rows.hpp -- degree-classed CSR row kernels with an in-order edge sum.
+//
+// The reference adds a row's edge terms to its force one after the other in
+// stored order (include/forceatlas.hpp:169-203, :415-467), so a row's sum is a
+// serial chain; but each TERM depends only on the two endpoints.  Rows are
+// therefore split by degree:
+//   light  (deg <= kMedDeg)    one thread per row, terms added as computed;
+//   medium (deg <= kHeavyDeg)  one wave per row: 64 terms at a time into LDS,
+//                              then every lane adds them in order (same chain,
+//                              broadcast reads);
+//   heavy                      one block per row, kHeavyU*256 terms per chunk.
+// A term computed alone is 0 + t, equal to t up to the sign of zero; the
+// accumulator starts at +0 and a round-to-nearest sum is -0 only when both
+// operands are, so it is never -0 and adding the stored term later gives the
+// reference's bits.
+//
+// One launch covers all three classes: blocks [0, nheavy) take heavy rows
+// (scheduled first: longest chains), then 4 medium rows per block, then 256
+// light rows per block.  `rows` lists heavy, then medium, then light rows.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace ge {
+
+constexpr int kRowT = 256;
+constexpr int kMedDeg = 32;
+constexpr int kHeavyDeg = 2048;
+constexpr int kHeavyU = 4;
+
+struct RowClasses {
+  const int* rows = nullptr;
+  int nheavy = 0, nmed = 0, nlight = 0;
+  int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
+};
+
+// Host: order `ids` (row ids with their degrees) into heavy, medium, light.
+inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
+                          std::vector<int>& out, int& nheavy, int& nmed, int& nlight) {
+  out.clear();
+  for (size_t q = 0; q < ids.size(); ++q)
+    if (deg[q] > kHeavyDeg) out.push_back(ids[q]);
+  nheavy = (int)out.size();
+  for (size_t q = 0; q < ids.size(); ++q)
+    if (deg[q] > kMedDeg && deg[q] <= kHeavyDeg) out.push_back(ids[q]);
+  nmed = (int)out.size() - nheavy;
+  for (size_t q = 0; q < ids.size(); ++q)
+    if (deg[q] <= kMedDeg) out.push_back(ids[q]);
+  nlight = (int)out.size() - nheavy - nmed;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int G>
+__device__ __forceinline__ void group_sync() {
+  if (G == 64)
+    wave_lds_sync();
+  else
+    __syncthreads();
+}
+
+// acc += term(e0) + term(e0+1) + ... in order; G threads (g = 0..G-1) share buf
+// (G*U*D doubles).  Every thread of the group ends with the same acc.
+template <int D, int G, int U, class Term>
+__device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* buf, Term&& term,
+                                                 double (&acc)[D]) {
+  for (int b = e0; b < e1; b += G * U) {
+    group_sync<G>();  // the previous chunk has been read by everyone
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = b + g + G * u;
+      if (e < e1) {
+        double t[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+        term(e, t);
+#pragma unroll
+        for (int k = 0; k < D; ++k) buf[(g + G * u) * D + k] = t[k];
+      }
+    }
+    group_sync<G>();
+    const int cnt = min(G * U, e1 - b);
+#pragma unroll 4
+    for (int l = 0; l < cnt; ++l)
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc[k] = acc[k] + buf[l * D + k];
+  }
+}
+
+// P: a row policy with
+//   struct State (holds acc[D] and the edge range e0, e1)
+//   load(row, State&), term(const State&, e, t[D]), finish(State&, bool writer).
+template <int D, class P>
+__global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) {
+  __shared__ double buf[kRowT * kHeavyU * D];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  typename P::State st;
+  if (b < L.nheavy) {
+    p.load(L.rows[b], st);
+    ordered_edge_sum<D, kRowT, kHeavyU>(
+        st.e0, st.e1, tid, buf, [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
+    p.finish(st, tid == 0);
+    return;
+  }
+  const int mblocks = (L.nmed + 3) / 4;
+  if (b < L.nheavy + mblocks) {
+    const int q = (b - L.nheavy) * 4 + (tid >> 6);
+    if (q >= L.nmed) return;  // wave-uniform; no block barrier on this path
+    const int lane = tid & 63;
+    p.load(L.rows[L.nheavy + q], st);
+    ordered_edge_sum<D, 64, 1>(
+        st.e0, st.e1, lane, buf + (tid >> 6) * 64 * D,
+        [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
+    p.finish(st, lane == 0);
+    return;
+  }
+  const int q = (b - L.nheavy - mblocks) * kRowT + tid;
+  if (q >= L.nlight) return;
+  p.load(L.rows[L.nheavy + L.nmed + q], st);
+  for (int e = st.e0; e < st.e1; ++e) {
+    double t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) t[k] = 0.0;
+    p.term(st, e, t);
+#pragma unroll
+    for (int k = 0; k < D; ++k) st.acc[k] = st.acc[k] + t[k];
+  }
+  p.finish(st, true);
+}
+
+}  // namespace ge

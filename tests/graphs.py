@@ -118,3 +118,17 @@ def random_coords(n, dim, seed=7):
 def as_lists(A):
     ip, ix, dx = A
     return [int(x) for x in ip], [int(x) for x in ix], [float(x) for x in dx]
+
+
+def with_hubs(A, hubs, seed=0):
+    """A plus stars: hub h joined to k distinct random vertices for (h, k) in
+    hubs (csr_from_edges symmetrises; unit weights).  Makes rows longer than one LDS chunk."""
+    n = len(A[0]) - 1
+    rows = np.repeat(np.arange(n), np.diff(A[0]))
+    src, dst = [rows], [A[1].astype(np.int64)]
+    rs = np.random.RandomState(seed)
+    for h, k in hubs:
+        nb = rs.choice(np.setdiff1d(np.arange(n), [h]), size=k, replace=False)
+        src.append(np.full(k, h))
+        dst.append(nb)
+    return csr_from_edges(n, np.concatenate(src), np.concatenate(dst))

@@ -61,6 +61,20 @@ def test_fa_tiled_kernel_bitexact(ctx, oracle, n, dim):
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=5), want)
 
 
+@pytest.mark.parametrize("use_weights", [1, 0])
+def test_fa_degree_classes(ctx, oracle, use_weights):
+    """Rows of every degree class of the attraction kernel (ge_rows.hpp): light,
+    wave-per-row (> 32 edges) and block-per-row (> 2048 edges, several chunks)."""
+    A = G.with_hubs(G.rmat(6000, 30000, seed=11), [(5, 4500), (17, 2100), (900, 300)])
+    A = (A[0], A[1], np.random.RandomState(2).uniform(0.5, 2.0, len(A[1])))
+    deg = np.diff(A[0])
+    assert deg.max() > 4096 and ((deg > 32) & (deg <= 2048)).any()
+    X0 = G.random_coords(len(deg), 3, seed=4)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=4, use_weights=use_weights)
+    got = ctx.force_atlas(A, 3, coords=X0, iterations=4, use_weights=use_weights)
+    assert np.array_equal(got, want)
+
+
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
     # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
@@ -176,8 +190,8 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R):
     monkeypatch.setenv("GE_FAML_R", str(R))
     sizes = [3000, 700, 2203, 90, 1]
     n = sum(sizes)
-    A = G.submatrix(G.rmat(n, 10 * n, seed=7), np.arange(n))
-    assert np.diff(A[0]).max() > 128
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=7), [(3, 2600), (40, 5000)], seed=R)
+    assert np.diff(A[0]).max() > 4096
     PT = _block_partition(n, sizes, seed=3)
     vA = ge.vertex_of(PT)
     m = len(sizes)
