@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <vector>
 
@@ -330,60 +331,173 @@ struct FaRows {
 };
 
 // ---------------------------------------------------------------------------
-// Small graphs: one workgroup runs every iteration, coordinates in LDS.
+// Small graphs (the coarsest level's 1e5 iterations, src/embed.cpp:586): one
+// 1024-thread workgroup runs every iteration, coordinates in LDS.  Row i is
+// owned by a group of G lanes: the G lanes evaluate the terms of G consecutive
+// partners (or CSR entries) at once, and the group's first lane adds them in
+// order -- the reference's serial sum, with G times the parallelism of one
+// lane per row (n = 127 gives 16 waves instead of 2).
 
-constexpr int kSmallMax = 1024;
+constexpr int kSmallMax = 512;  // one row group per thread group below
+constexpr int kSmallT = 512;
+constexpr int kSmallNnz = 6144;
 
-template <int D>
-__global__ void __launch_bounds__(256)
-fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
-                const double* __restrict__ dx, const double* __restrict__ dp1g,
+// The G lanes of a group hold U terms each (term u of lane g is partner
+// g + G*u of the chunk); the group's first lane adds the first cnt in order.
+template <int D, int G, int U>
+__device__ __forceinline__ void group_add(const double (&t)[U][D], int tid, int g, int cnt,
+                                          bool leader, double* __restrict__ tb,
+                                          double (&acc)[D]) {
+  if (G == 1) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < cnt)
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[u][k];
+    return;
+  }
+  const int base = tid - g;  // the group's first lane
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int k = 0; k < D; ++k) tb[(base * U + g + G * u) * D + k] = t[u][k];
+  wave_lds_sync();
+  if (leader) {
+    constexpr int B = (G * U < 8) ? G * U : 8;  // terms read ahead of the ordered adds
+#pragma unroll
+    for (int l0 = 0; l0 < G * U; l0 += B) {
+      double v[B][D];
+#pragma unroll
+      for (int l = 0; l < B; ++l)
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[l][k] = tb[(base * U + l0 + l) * D + k];
+#pragma unroll
+      for (int l = 0; l < B; ++l)
+        if (l0 + l < cnt)
+#pragma unroll
+          for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[l][k];
+    }
+  }
+  wave_lds_sync();
+}
+
+// STAGED: the CSR indices and weights (nnz <= kSmallNnz) are copied to LDS once.
+template <int D, int G, int U, bool STAGED>
+__global__ void __launch_bounds__(kSmallT)
+fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
+                const double* __restrict__ dxg, const double* __restrict__ dp1g,
                 double* __restrict__ Xg, int iterations, FaConst c) {
   constexpr int W = Rec<D>::W;
-  constexpr int RM = kSmallMax / 256;
   __shared__ __attribute__((aligned(16))) double sx[kSmallMax * W];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < n; i += 256) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) sx[i * W + k] = Xg[(size_t)i * D + k];
-    sx[i * W + D] = dp1g[i];
+  __shared__ double tb[(G > 1 ? kSmallT * U : 1) * D];
+  __shared__ int s_ix[STAGED ? kSmallNnz : 1];
+  __shared__ double s_dx[STAGED ? kSmallNnz : 1];
+  if (STAGED) {
+    for (int e = threadIdx.x; e < ip[n]; e += kSmallT) {
+      s_ix[e] = ixg[e];
+      s_dx[e] = dxg[e];
+    }
   }
-  double fprev[RM][D], F[RM][D];
+  const int* __restrict__ ix = STAGED ? s_ix : ixg;
+  const double* __restrict__ dx = STAGED ? s_dx : dxg;
+  const int tid = threadIdx.x;
+  const int g = tid % G;
+  const int i = tid / G;
+  const bool active = i < n;
+  const bool leader = active && g == 0;
+  for (int q = tid; q < n; q += kSmallT) {
 #pragma unroll
-  for (int r = 0; r < RM; ++r)
+    for (int k = 0; k < D; ++k) sx[q * W + k] = Xg[(size_t)q * D + k];
+    sx[q * W + D] = dp1g[q];
+  }
+  const int e0 = active ? ip[i] : 0;
+  const int e1 = active ? ip[i + 1] : 0;
+  double fprev[D], F[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) fprev[r][k] = 0.0;
+  for (int k = 0; k < D; ++k) fprev[k] = F[k] = 0.0;
 
   for (int it = 0; it < iterations; ++it) {
     __syncthreads();
+    double xi[D], acc[D];
 #pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      const int i = tid + r * 256;
-      if (i >= n) break;
-      double xi[D], acc[D];
+    for (int k = 0; k < D; ++k) {
+      xi[k] = active ? sx[i * W + k] : 0.0;
+      acc[k] = 0.0;
+    }
+    const double dip1 = active ? sx[i * W + D] : 1.0;
+    const bool row_ok = all_coord_ok<D>(xi);
+    const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
+    // every row in the shared-reciprocal domain: branch-free pair and edge
+    // bodies the compiler can interleave across the U terms of a lane
+    if (__syncthreads_and(!active || rep_ok)) {
+      for (int j0 = 0; j0 < n; j0 += G * U) {  // :151-167, j ascending
+        double t[U][D];
 #pragma unroll
-      for (int k = 0; k < D; ++k) {
-        xi[k] = sx[i * W + k];
-        acc[k] = 0.0;
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + g + G * u;
+          const int jj = min(j, n - 1);
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+          rep_pair<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t[u]);
+          if (j >= n)
+#pragma unroll
+            for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+        }
+        group_add<D, G, U>(t, tid, g, min(G * U, n - j0), leader, tb, acc);
       }
-      const double dip1 = sx[i * W + D];
-      const bool row_ok = all_coord_ok<D>(xi);
-      const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
-      for (int j = 0; j < n; ++j) {
-        const double* xj = &sx[j * W];
-        if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
-          rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, acc);
-        else
-          rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, acc);
+      for (int b = e0; b < e1; b += G * U) {  // :169-203, CSR order
+        double t[U][D];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = b + g + G * u;
+          const int ee = min(e, e1 - 1);
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+          attr_edge<D, true>(xi, &sx[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, dip1, c, t[u]);
+          if (e >= e1)
+#pragma unroll
+            for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+        }
+        group_add<D, G, U>(t, tid, g, min(G * U, e1 - b), leader, tb, acc);
       }
-      for (int e = ip[i]; e < ip[i + 1]; ++e) {
-        const double* xj = &sx[ix[e] * W];
-        const double a = c.use_weights ? dx[e] : 1.0;
-        if (row_ok && all_coord_ok<D>(xj))
-          attr_edge<D, true>(xi, xj, a, dip1, c, acc);
-        else
-          attr_edge<D, false>(xi, xj, a, dip1, c, acc);
+    } else {
+    for (int j0 = 0; j0 < n; j0 += G * U) {  // :151-167, j ascending
+      double t[U][D];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + g + G * u;
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+        if (active && j < n) {
+          const double* xj = &sx[j * W];
+          if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
+            rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+          else
+            rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+        }
       }
+      group_add<D, G, U>(t, tid, g, min(G * U, n - j0), leader, tb, acc);
+    }
+    for (int b = e0; b < e1; b += G * U) {  // :169-203, CSR order
+      double t[U][D];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = b + g + G * u;
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+        if (e < e1) {
+          const double* xj = &sx[ix[e] * W];
+          const double a = c.use_weights ? dx[e] : 1.0;
+          if (row_ok && all_coord_ok<D>(xj))
+            attr_edge<D, true>(xi, xj, a, dip1, c, t[u]);
+          else
+            attr_edge<D, false>(xi, xj, a, dip1, c, t[u]);
+        }
+      }
+      group_add<D, G, U>(t, tid, g, min(G * U, e1 - b), leader, tb, acc);
+    }
+    }
+    if (leader) {  // gravity :205-211 (mag not clamped)
       double m2 = xi[0] * xi[0];
 #pragma unroll
       for (int k = 1; k < D; ++k) m2 = m2 + xi[k] * xi[k];
@@ -391,19 +505,16 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
       double unit[D];
       neg_over<D>(xi, mag, unit);
 #pragma unroll
-      for (int k = 0; k < D; ++k) F[r][k] = acc[k] + unit[k] * c.gravity * dip1;
+      for (int k = 0; k < D; ++k) F[k] = acc[k] + unit[k] * c.gravity * dip1;
     }
     __syncthreads();
-#pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      const int i = tid + r * 256;
-      if (i >= n) break;
+    if (leader) {  // swing + update :214-269
       double s = 0.0, f2 = 0.0;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        const double t = fprev[r][k] - F[r][k];
+        const double t = fprev[k] - F[k];
         s = (k == 0) ? t * t : s + t * t;
-        f2 = (k == 0) ? F[r][k] * F[r][k] : f2 + F[r][k] * F[r][k];
+        f2 = (k == 0) ? F[k] * F[k] : f2 + F[k] * F[k];
       }
       const double swing = sqrt(s);
       const double totalF = sqrt(f2);
@@ -412,15 +523,50 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ix,
       if (speed > cap) speed = cap;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        sx[i * W + k] = F[r][k] * speed + sx[i * W + k];
-        fprev[r][k] = F[r][k];
+        sx[i * W + k] = F[k] * speed + sx[i * W + k];
+        fprev[k] = F[k];
       }
     }
   }
   __syncthreads();
-  for (int i = tid; i < n; i += 256)
+  for (int q = tid; q < n; q += kSmallT)
 #pragma unroll
-    for (int k = 0; k < D; ++k) Xg[(size_t)i * D + k] = sx[i * W + k];
+    for (int k = 0; k < D; ++k) Xg[(size_t)q * D + k] = sx[q * W + k];
+}
+
+// lanes per row for n rows in one 1024-thread workgroup
+inline int small_group(int n) {
+  if (const char* e = std::getenv("GE_SMALL_G")) {  // tuning override
+    const int g = std::atoi(e);
+    if ((g == 1 || g == 2 || g == 4 || g == 8 || g == 16) && n * g <= kSmallT) return g;
+  }
+  int G = 1;
+  while (G < 16 && n * G * 2 <= kSmallT) G *= 2;
+  return G;
+}
+
+template <int D>
+void launch_small(hipStream_t s, int n, int nnz, const int* ip, const int* ix, const double* dx,
+                  const double* dp1, double* X, int iterations, const FaConst& c) {
+  const bool staged = nnz <= kSmallNnz;
+  switch (small_group(n) * 2 + (staged ? 1 : 0)) {
+#define GE_SMALL(GG, ST)                                                                    \
+  case GG * 2 + ST:                                                                         \
+    hipLaunchKernelGGL((fa_small_strict<D, GG, 1, ST == 1>), dim3(1), dim3(kSmallT), 0, s, n, \
+                       ip, ix, dx, dp1, X, iterations, c);                                  \
+    break;
+    GE_SMALL(1, 0)
+    GE_SMALL(2, 0)
+    GE_SMALL(4, 0)
+    GE_SMALL(8, 0)
+    GE_SMALL(16, 0)
+    GE_SMALL(1, 1)
+    GE_SMALL(2, 1)
+    GE_SMALL(4, 1)
+    GE_SMALL(8, 1)
+    GE_SMALL(16, 1)
+#undef GE_SMALL
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -568,8 +714,7 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
     FaConst c = make_const(p);
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
-      hipLaunchKernelGGL((fa_small_strict<D>), dim3(1), dim3(256), 0, s, n, d_ip, d_ix, d_dx,
-                         dp1.p, d_x, iterations, c);
+      launch_small<D>(s, n, nnz, d_ip, d_ix, d_dx, dp1.p, d_x, iterations, c);
     });
     GE_HIP(hipGetLastError());
     GE_HIP(hipStreamSynchronize(s));

@@ -546,25 +546,37 @@ int ge_embed(ge_ctx* ctx, int levels, const int* a_n, const int* a_off, const in
       GE_REQUIRE(Pip(l)[p_rows[l]] == a_n[l], "As[l].Rows() must equal P_Ts[l].Cols()");
 
     const int L = levels;
+    const bool prof = std::getenv("GE_PROFILE_EMBED") != nullptr;
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
     if (print_progress) std::cout << "embedding layer " << L + 1 << ": getting base coords" << std::endl;
     std::vector<double> coarse((size_t)a_n[L] * dim);
+    auto t0 = clk();
     ge::fa_host(ctx, a_n[L], Aip(L), Aix(L), Adx(L), dim, coarse.data(), true, base_iterations, p);
+    if (prof)
+      std::fprintf(stderr, "embed: coarsest forceAtlas n=%d %d iterations %.3fs\n", a_n[L],
+                   base_iterations, secs(t0, clk()));
     std::vector<double> r_coarse, cAc;
     for (int l = L - 1; l >= 0; --l) {
       if (print_progress) std::cout << "embeding layer " << l + 1 << std::endl;  // sic (:613)
       const int m = a_n[l + 1];
       const bool base = (l + 1 == L);
       std::vector<double> rA(m);
+      auto t1 = clk();
       ge::radius_step(m, coarse.data(), rA.data(), dim, base, base ? 0 : p_rows[l + 1],
                       base ? nullptr : Pip(l + 1), base ? nullptr : Pix(l + 1),
                       base ? nullptr : cAc.data(), base ? nullptr : r_coarse.data(), Aip(l + 1),
                       Aix(l + 1));
+      auto t2 = clk();
       std::vector<int> vA(a_n[l]);
       for (int a = 0; a < m; ++a)
         for (int c = Pip(l)[a]; c < Pip(l)[a + 1]; ++c) vA[Pix(l)[c]] = a;
       std::vector<double> fine((size_t)a_n[l] * dim, 0.0);
       ge::faml_host(ctx, a_n[l], Aip(l), Aix(l), Adx(l), m, Pip(l), Pix(l), vA.data(),
                     coarse.data(), rA.data(), fine.data(), dim, ml_iterations, p);
+      if (prof)
+        std::fprintf(stderr, "embed: level %d n=%d: radius step %.3fs, forceAtlasMultilevel %.3fs\n",
+                     l, a_n[l], secs(t1, t2), secs(t2, clk()));
       cAc = std::move(coarse);
       r_coarse = std::move(rA);
       coarse = std::move(fine);
