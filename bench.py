@@ -71,17 +71,18 @@ def pmc_traffic_per_launch(kernel_prefix):
     MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a wide coalesced
     read -> bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024."""
     def read(pattern, counter):
-        files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", pattern)))
-        if not files:
-            return None
         import csv
-        vals = []
-        with open(files[-1]) as f:
-            for row in csv.DictReader(f):
-                if row.get("Counter_Name") == counter and row.get("Kernel_Name", "").find(
-                        kernel_prefix) >= 0:
-                    vals.append(float(row["Counter_Value"]))
-        return (sum(vals) / len(vals), files[-1]) if vals else None
+        # newest round directory first; the first file that traced this kernel wins
+        for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", pattern)), reverse=True):
+            vals = []
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if row.get("Counter_Name") == counter and row.get("Kernel_Name", "").find(
+                            kernel_prefix) >= 0:
+                        vals.append(float(row["Counter_Value"]))
+            if vals:
+                return sum(vals) / len(vals), path
+        return None
     f = read("pmc_fetch*.csv", "FETCH_SIZE")
     w = read("pmc_write*.csv", "WRITE_SIZE")
     if not f or not w:
@@ -209,12 +210,16 @@ def run_c3(args, rank, world, local, dev):
     elapsed = time.perf_counter() - t0
     run_ms = e0.elapsed_time(e1) / args.steps
     res_ms, str_ms, _ = plan.kernel_ms()
+    rep_ms, rep_launches, rep_pairs = plan.repulse_ms()
+    traffic, traffic_src = pmc_traffic_per_launch("faml_big_repulse")
     finite = bool(torch.isfinite(X).all().item())
     sizes = np.diff(PT[0]).astype(np.float64)
     pairs = float((sizes * (sizes - 1)).sum())
     flops = FLOPS_PER_PAIR * pairs * args.ml_iterations
     its = args.steps * args.ml_iterations / elapsed
-    tflops = flops / (run_ms * 1e-3) / 1e12
+    tflops = flops / (run_ms * 1e-3) / 1e12  # whole level, all kernels
+    rep_flops = FLOPS_PER_PAIR * rep_pairs
+    rep_tflops = rep_flops / (rep_ms * 1e-3) / 1e12 if rep_ms > 0 else 0.0
     result = {
         "metric": METRIC, "value": its, "unit": "iterations/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
@@ -230,12 +235,15 @@ def run_c3(args, rank, world, local, dev):
         "pair_interactions_per_s": pairs * its,
         "finite": finite,
         "setup_seconds": {"graph": t_gen, "partition_host": t_part, "ptap_device": t_ptap},
-        "roofline": {"kernel": "faml_resident + faml_huge (in-aggregate all-pairs, fp64)",
+        "roofline": {"kernel": "faml_big_repulse (streamed in-aggregate all-pairs, fp64)",
                      "bound": "mfma", "pipe": "fp64 VALU (dense FP64 peak 78.6 TFLOP/s, spec)",
-                     "achieved": tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": tflops / FP64_PEAK_TFLOPS, "traffic": None,
-                     "flops_per_launch": flops, "avg_launch_ms": run_ms,
-                     "resident_ms": res_ms, "streamed_ms": str_ms},
+                     "achieved": rep_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": rep_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src, "flops_per_launch": rep_flops,
+                     "avg_launch_ms": rep_ms, "launches": rep_launches},
+        "level_rate": {"flops_per_step": flops, "ms_per_step_device": run_ms,
+                       "tflops_all_kernels": tflops, "resident_ms": res_ms,
+                       "streamed_ms": str_ms},
     }
     if args.end_to_end:
         t0 = time.perf_counter()
@@ -347,7 +355,7 @@ def main():
     attr_bytes = 12 * nnz * rows / n + 52 * rows + 4  # SURVEY 8(d) B_attr, this rank's rows
     att_gbs = attr_bytes / (att_ms * 1e-3) / 1e9 if att_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic_per_launch("fa_repulse")
-    att_traffic, _ = pmc_traffic_per_launch("fa_attract_update")
+    att_traffic, _ = pmc_traffic_per_launch("FaRows")
 
     result = {
         "metric": METRIC,
@@ -387,7 +395,7 @@ def main():
             "launches": launches,
         },
         "roofline_attraction": {
-            "kernel": "fa_attract_update_strict (CSR attraction + gravity + update)",
+            "kernel": "classed_rows_kernel<FaRows> (CSR attraction + gravity + update)",
             "bound": "hbm",
             "achieved": att_gbs,
             "peak": HBM_PEAK_GBS,
@@ -402,20 +410,6 @@ def main():
         result["cpu_baseline"] = cpu_baseline(A, X0, args.dim, args.cpu_baseline_seconds, rank)
         result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
     plan.close()
-    if args.sweep_slots:  # streamed-path row slots per lane (tuning aid, stderr only)
-        for R in (1, 2, 4):
-            os.environ["GE_FAML_R"] = str(R)
-            p2 = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
-                             PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
-                             args.dim, iterations=args.ml_iterations)
-            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
-            torch.cuda.synchronize(dev)
-            t0 = time.perf_counter()
-            p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
-            torch.cuda.synchronize(dev)
-            log(rank, f"sweep R={R}: {1e3 * (time.perf_counter() - t0):.1f} ms per call")
-            p2.close()
-        os.environ.pop("GE_FAML_R")
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

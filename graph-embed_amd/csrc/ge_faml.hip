@@ -617,6 +617,7 @@ struct ge_faml_plan {
   ge::RowClasses ecls;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, rep_blocks = 0;
+  double streamed_pairs = 0.0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
   // the size classes are independent: streamed path, large, mid and small
   // packs each run on their own stream and join the context stream at the end
@@ -625,6 +626,8 @@ struct ge_faml_plan {
   bool profiling = false;
   std::vector<hipEvent_t> ev;  // 4 per timed run: start, resident end, streamed start/end
   size_t next_ev = 0;
+  std::vector<hipEvent_t> rev;  // 2 per profiled repulsion launch
+  size_t next_rev = 0;
 };
 
 namespace ge {
@@ -714,6 +717,10 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
   std::vector<int2> items;
   for (const Item& it : its) items.push_back(make_int2(it.a, it.r0));
   pl->R = R;
+  for (int a : big) {
+    const double sa = h_pt_ip[a + 1] - h_pt_ip[a];
+    pl->streamed_pairs += sa * (sa - 1);
+  }
   pl->rep_blocks = cus * rep_occupancy(dim, R);
   std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
@@ -792,8 +799,21 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
+        hipEvent_t* re = nullptr;
+        if (pl->profiling) {
+          if (pl->next_rev + 2 > pl->rev.size())
+            for (int k = 0; k < 256; ++k) {
+              hipEvent_t e;
+              GE_HIP(hipEventCreate(&e));
+              pl->rev.push_back(e);
+            }
+          re = &pl->rev[pl->next_rev];
+          pl->next_rev += 2;
+          GE_HIP(hipEventRecord(re[0], ss));
+        }
         launch_big_repulse<D>(pl->R, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                               pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
+        if (re) GE_HIP(hipEventRecord(re[1], ss));
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx,
                              cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
         hipLaunchKernelGGL((classed_rows_kernel<D, FamlRows<D>>), dim3(pl->ecls.grid()),
@@ -838,6 +858,7 @@ static void faml_plan_free(ge_faml_plan* pl) {
   }
   if (pl->fork) (void)hipEventDestroy(pl->fork);
   for (hipEvent_t e : pl->ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : pl->rev) (void)hipEventDestroy(e);
   delete pl;
 }
 
@@ -923,6 +944,7 @@ int ge_faml_plan_set_profiling(ge_faml_plan* pl, int enable) {
     GE_REQUIRE(pl, "null plan");
     pl->profiling = enable != 0;
     pl->next_ev = 0;
+    pl->next_rev = 0;
   });
 }
 
@@ -945,6 +967,25 @@ int ge_faml_plan_kernel_ms(ge_faml_plan* pl, double* resident_ms, double* stream
     *resident_ms = cnt ? a / cnt : 0.0;
     *streamed_ms = cnt ? b / cnt : 0.0;
     *runs = cnt;
+  });
+}
+
+int ge_faml_plan_repulse_ms(ge_faml_plan* pl, double* ms, int* launches, double* pairs) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && ms && launches && pairs, "null argument");
+    *pairs = pl->streamed_pairs;
+    ge::DeviceGuard g(pl->ctx);
+    GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+    double t = 0;
+    int cnt = 0;
+    for (size_t k = 0; k + 2 <= pl->next_rev; k += 2) {
+      float x = 0.f;
+      GE_HIP(hipEventElapsedTime(&x, pl->rev[k], pl->rev[k + 1]));
+      t += x;
+      ++cnt;
+    }
+    *ms = cnt ? t / cnt : 0.0;
+    *launches = cnt;
   });
 }
 

@@ -98,6 +98,8 @@ _SIGS = {
     "ge_faml_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ge_faml_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double), _ip]),
+    "ge_faml_plan_repulse_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _ip,
+                                               ctypes.POINTER(ctypes.c_double)]),
     "ge_faml_plan_destroy": (ctypes.c_int, [_vp]),
     "ge_selftest_math": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_ulonglong,
                                         ctypes.POINTER(ctypes.c_longlong)]),
@@ -272,6 +274,14 @@ class FamlPlan:
         _check(lib().ge_faml_plan_kernel_ms(self.h, ctypes.byref(a), ctypes.byref(b),
                                             ctypes.byref(c)))
         return a.value, b.value, c.value
+
+    def repulse_ms(self):
+        """(average ms of one streamed repulsion launch, launches profiled,
+        ordered pairs per launch)"""
+        a, c, p = ctypes.c_double(), ctypes.c_int(), ctypes.c_double()
+        _check(lib().ge_faml_plan_repulse_ms(self.h, ctypes.byref(a), ctypes.byref(c),
+                                             ctypes.byref(p)))
+        return a.value, c.value, p.value
 
     def close(self):
         if self.h:

@@ -115,6 +115,11 @@ int ge_faml_plan_set_profiling(ge_faml_plan* plan, int enable);
 /* Average device ms of the resident (LDS) kernels and of the streamed path per run. */
 int ge_faml_plan_kernel_ms(ge_faml_plan* plan, double* resident_ms, double* streamed_ms,
                            int* runs);
+/* Average device ms of one streamed-path repulsion launch (faml_big_repulse, one
+ * per iteration) over the profiled runs, and the ordered pairs one launch
+ * evaluates (sum of s(s-1) over the streamed aggregates); 0 launches if none. */
+int ge_faml_plan_repulse_ms(ge_faml_plan* plan, double* ms_per_launch, int* launches,
+                            double* pairs_per_launch);
 int ge_faml_plan_destroy(ge_faml_plan* plan);
 
 /* ---- coarsening hierarchy ----
