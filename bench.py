@@ -191,23 +191,44 @@ def run_c3(args, rank, world, local, dev):
     work = torch.cuda.Stream(dev)
     torch.cuda.set_stream(work)
     ctx.set_stream(work.cuda_stream)
+    torch.cuda.synchronize(dev)  # inputs and X's fill are done before the work stream runs
+    # aggregates dealt to ranks by cost (LPT); no collective inside the 100
+    # iterations, one member all-gather per call
+    from ge_amd.dist import aggregate_cost, assign_aggregates, member_rows, allgather_members
+    owned, loads = assign_aggregates(aggregate_cost(PT[0], L[0], PT[1]), world)
+    rows = [member_rows(PT[0], PT[1], o) for o in owned]
+    log(rank, f"aggregate shards: loads {[f'{x:.3g}' for x in loads]}")
     plan = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
                        PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
-                       args.dim, iterations=args.ml_iterations)
-    run = lambda: plan.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(),  # noqa
-                           X.data_ptr())
+                       args.dim, iterations=args.ml_iterations,
+                       aggs=owned[rank] if world > 1 else None)
+
+    def run():
+        plan.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+        allgather_members(X, rows, rank, world)
+
+    import torch.distributed as dist
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize(dev)
     plan.set_profiling(True)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     e0.record()
     for _ in range(args.steps):
         run()
     e1.record()
     torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
     run_ms = e0.elapsed_time(e1) / args.steps
     res_ms, str_ms, _ = plan.kernel_ms()
     rep_ms, rep_launches, rep_pairs = plan.repulse_ms()
@@ -230,7 +251,8 @@ def run_c3(args, rank, world, local, dev):
                                f"Graph500 R-MAT ({args.n} ids, {args.draws} draws), "
                                "partition(A, 0.125) first 4 levels, strict fp64",
                    "n": n0, "nnz": nnz0, "aggregates": m, "dim": args.dim,
-                   "levels": [h[2] for h in hier], "parallelism": "aggregates1"},
+                   "levels": [h[2] for h in hier],
+                   "parallelism": f"aggregates{world}" + ("+member-allgather" if world > 1 else "")},
         "edges_per_s": nnz0 * its,
         "pair_interactions_per_s": pairs * its,
         "finite": finite,
@@ -317,6 +339,7 @@ def main():
     work = torch.cuda.Stream(dev)
     torch.cuda.set_stream(work)
     ctx.set_stream(work.cuda_stream)
+    torch.cuda.synchronize(dev)  # the coordinate upload is done before the work stream runs
     mode = ge.MODE_FAST if args.mode == "fast" else ge.MODE_STRICT
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), args.dim, rb, re,
                        mode=mode)

@@ -632,7 +632,8 @@ struct ge_faml_plan {
 
 namespace ge {
 
-static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1) {
+// aggs: the aggregates this plan runs (strictly increasing ids).
+static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vector<int>& aggs) {
   hipStream_t st = pl->ctx->stream;
   const int dim = pl->dim;
   // Work of aggregate a per iteration ~ s^2.  Aggregates whose share would
@@ -640,7 +641,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
   // streamed path (many blocks per aggregate, one launch per iteration);
   // the rest stay resident in LDS for all iterations.
   double W = 0.0;
-  for (int a = a0; a < a1; ++a) {
+  for (int a : aggs) {
     const double s = h_pt_ip[a + 1] - h_pt_ip[a];
     W += s * s;
   }
@@ -652,7 +653,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, int a0, int a1
   split = std::max(256, std::min(split, large_cap(dim)));
 
   std::vector<int> small, mid, large, big;
-  for (int a = a0; a < a1; ++a) {
+  for (int a : aggs) {
     const int s = h_pt_ip[a + 1] - h_pt_ip[a];
     if (s <= 0) continue;
     if (s <= 64) small.push_back(a);
@@ -882,7 +883,9 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
     pl->pt_ix = d_pt_ix;
     pl->vA = d_vA;
     pl->c = make_fa_const(p);
-    faml_plan_build(pl, h_pt_ip, 0, m);
+    std::vector<int> all(m);
+    std::iota(all.begin(), all.end(), 0);
+    faml_plan_build(pl, h_pt_ip, all);
     faml_plan_run(pl, d_cA, d_rA, d_init, d_x);
     GE_HIP(hipStreamSynchronize(ctx->stream));
   } catch (...) {
@@ -896,16 +899,12 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
 
 extern "C" {
 
-int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
-                        int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
-                        const int* d_vA, int dim, const ge_fa_params* p, int iterations,
-                        int agg_begin, int agg_end, ge_faml_plan** out) {
+static int faml_plan_create_impl(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix,
+                                 const double* d_dx, int m, const int* h_pt_ip,
+                                 const int* d_pt_ip, const int* d_pt_ix, const int* d_vA,
+                                 int dim, const ge_fa_params* p, int iterations,
+                                 const std::vector<int>& aggs, ge_faml_plan** out) {
   return ge::guarded([&] {
-    GE_REQUIRE(ctx && p && out && h_pt_ip, "null argument");
-    GE_REQUIRE(dim >= 1 && dim <= 4, "dimension must be 1..4");
-    GE_REQUIRE(n > 0 && m > 0 && h_pt_ip[0] == 0 && h_pt_ip[m] == n,
-               "P_T must have one entry per fine vertex");
-    GE_REQUIRE(0 <= agg_begin && agg_begin <= agg_end && agg_end <= m, "bad aggregate range");
     ge::DeviceGuard g(ctx);
     auto* pl = new ge_faml_plan();
     try {
@@ -921,13 +920,56 @@ int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, co
       pl->pt_ix = d_pt_ix;
       pl->vA = d_vA;
       pl->c = ge::make_fa_const(*p);
-      ge::faml_plan_build(pl, h_pt_ip, agg_begin, agg_end);
+      ge::faml_plan_build(pl, h_pt_ip, aggs);
     } catch (...) {
       ge::faml_plan_free(pl);
       throw;
     }
     *out = pl;
   });
+}
+
+static void faml_plan_check(ge_ctx* ctx, int n, int m, const int* h_pt_ip, int dim,
+                            const ge_fa_params* p, void* out) {
+  GE_REQUIRE(ctx && p && out && h_pt_ip, "null argument");
+  GE_REQUIRE(dim >= 1 && dim <= 4, "dimension must be 1..4");
+  GE_REQUIRE(n > 0 && m > 0 && h_pt_ip[0] == 0 && h_pt_ip[m] == n,
+             "P_T must have one entry per fine vertex");
+}
+
+int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
+                        int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
+                        const int* d_vA, int dim, const ge_fa_params* p, int iterations,
+                        int agg_begin, int agg_end, ge_faml_plan** out) {
+  std::vector<int> aggs;
+  const int rc = ge::guarded([&] {
+    faml_plan_check(ctx, n, m, h_pt_ip, dim, p, out);
+    GE_REQUIRE(0 <= agg_begin && agg_begin <= agg_end && agg_end <= m, "bad aggregate range");
+    aggs.resize(agg_end - agg_begin);
+    std::iota(aggs.begin(), aggs.end(), agg_begin);
+  });
+  if (rc != GE_OK) return rc;
+  return faml_plan_create_impl(ctx, n, d_ip, d_ix, d_dx, m, h_pt_ip, d_pt_ip, d_pt_ix, d_vA, dim,
+                               p, iterations, aggs, out);
+}
+
+int ge_faml_plan_create_subset(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix,
+                               const double* d_dx, int m, const int* h_pt_ip,
+                               const int* d_pt_ip, const int* d_pt_ix, const int* d_vA, int dim,
+                               const ge_fa_params* p, int iterations, const int* h_aggs,
+                               int n_aggs, ge_faml_plan** out) {
+  std::vector<int> aggs;
+  const int rc = ge::guarded([&] {
+    faml_plan_check(ctx, n, m, h_pt_ip, dim, p, out);
+    GE_REQUIRE(n_aggs >= 0 && (h_aggs || n_aggs == 0), "bad aggregate list");
+    for (int q = 0; q < n_aggs; ++q)
+      GE_REQUIRE(h_aggs[q] >= 0 && h_aggs[q] < m && (q == 0 || h_aggs[q] > h_aggs[q - 1]),
+                 "aggregate ids must be strictly increasing and < m");
+    aggs.assign(h_aggs, h_aggs + n_aggs);
+  });
+  if (rc != GE_OK) return rc;
+  return faml_plan_create_impl(ctx, n, d_ip, d_ix, d_dx, m, h_pt_ip, d_pt_ip, d_pt_ix, d_vA, dim,
+                               p, iterations, aggs, out);
 }
 
 int ge_faml_plan_run(ge_faml_plan* pl, const double* d_cA, const double* d_rA,

@@ -94,6 +94,10 @@ _SIGS = {
                                            _vp, _vp, _vp, ctypes.c_int, ctypes.POINTER(FaParams),
                                            ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_vp)]),
+    "ge_faml_plan_create_subset": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int,
+                                                  _i32p, _vp, _vp, _vp, ctypes.c_int,
+                                                  ctypes.POINTER(FaParams), ctypes.c_int, _i32p,
+                                                  ctypes.c_int, ctypes.POINTER(_vp)]),
     "ge_faml_plan_run": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "ge_faml_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ge_faml_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
@@ -251,16 +255,25 @@ class FamlPlan:
     (pt_indptr_host, numpy) plus device pointers for everything else."""
 
     def __init__(self, ctx, n, d_ip, d_ix, d_dx, pt_indptr_host, d_pt_ip, d_pt_ix, d_vA, dim,
-                 iterations=100, agg_range=None, **kw):
+                 iterations=100, agg_range=None, aggs=None, **kw):
+        """agg_range=(a0, a1) or aggs=(strictly increasing aggregate ids) restricts
+        the plan to those aggregates (one rank's share); default: all."""
         self.ctx = ctx
         pip = np.ascontiguousarray(pt_indptr_host, dtype=np.int32)
         m = len(pip) - 1
-        a0, a1 = agg_range if agg_range else (0, m)
         p = params(**kw)
         h = _vp()
-        _check(lib().ge_faml_plan_create(ctx.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip,
-                                         _vp(d_pt_ip), _vp(d_pt_ix), _vp(d_vA), dim,
-                                         ctypes.byref(p), iterations, a0, a1, ctypes.byref(h)))
+        if aggs is not None:
+            ids = np.ascontiguousarray(aggs, dtype=np.int32)
+            _check(lib().ge_faml_plan_create_subset(
+                ctx.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip, _vp(d_pt_ip), _vp(d_pt_ix),
+                _vp(d_vA), dim, ctypes.byref(p), iterations, ids, len(ids), ctypes.byref(h)))
+        else:
+            a0, a1 = agg_range if agg_range else (0, m)
+            _check(lib().ge_faml_plan_create(ctx.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip,
+                                             _vp(d_pt_ip), _vp(d_pt_ix), _vp(d_vA), dim,
+                                             ctypes.byref(p), iterations, a0, a1,
+                                             ctypes.byref(h)))
         self.h = h
 
     def run(self, d_cA, d_rA, d_init, d_x):

@@ -109,6 +109,15 @@ int ge_faml_plan_create(ge_ctx* ctx, int n, const int* d_indptr, const int* d_in
                         const int* d_pt_indptr, const int* d_pt_indices, const int* d_vertex_A,
                         int dim, const ge_fa_params* p, int iterations, int agg_begin,
                         int agg_end, ge_faml_plan** out);
+/* The same for an arbitrary set of aggregates (h_aggs: n_aggs strictly increasing
+ * ids) -- one rank's share when aggregates are dealt to GPUs by cost
+ * (ge_amd.dist.assign_aggregates). */
+int ge_faml_plan_create_subset(ge_ctx* ctx, int n, const int* d_indptr, const int* d_indices,
+                               const double* d_data, int m, const int* h_pt_indptr,
+                               const int* d_pt_indptr, const int* d_pt_indices,
+                               const int* d_vertex_A, int dim, const ge_fa_params* p,
+                               int iterations, const int* h_aggs, int n_aggs,
+                               ge_faml_plan** out);
 int ge_faml_plan_run(ge_faml_plan* plan, const double* d_coords_A, const double* d_r_A,
                      const double* d_init, double* d_coords);
 int ge_faml_plan_set_profiling(ge_faml_plan* plan, int enable);

@@ -69,3 +69,57 @@ def test_row_shards_cover_exactly():
             assert sh[0][0] == 0 and sh[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
             assert chunk * world >= n
+
+
+# --------------------------------------------------------------------------
+# forceAtlasMultilevel sharded by aggregates (ge_amd.dist.assign_aggregates /
+# allgather_members): each rank produces only its aggregates' member rows (here
+# cut from the oracle's level result, standing in for its FamlPlan subset), the
+# member all-gather must rebuild the whole level on every rank.
+
+def _ml_worker(rank, world, port, PT, full, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ge_amd.dist import aggregate_cost, assign_aggregates, member_rows, allgather_members
+    owned, _ = assign_aggregates(aggregate_cost(PT[0]), world)
+    rows = [member_rows(PT[0], PT[1], o) for o in owned]
+    X = torch.zeros(full.shape, dtype=torch.float64)
+    mine = torch.as_tensor(rows[rank], dtype=torch.long)
+    X[mine] = torch.from_numpy(full)[mine]
+    allgather_members(X, rows, rank, world)
+    np.save(out_path % rank, X.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_aggregate_sharded_level_gather(oracle, tmp_path, world):
+    from ge_amd import vertex_of
+    A = G.largest_component(G.rmat(2000, 14000, seed=23))
+    PT = oracle.partition(A, 0.125)[0]
+    vA = vertex_of(PT)
+    m = PT[2]
+    cA = G.random_coords(m, 3, seed=1)
+    rA = np.random.RandomState(2).uniform(0.05, 0.3, m)
+    full = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=10, seed=4)
+    out = str(tmp_path / "x%d.npy")
+    mp.start_processes(_ml_worker, args=(world, _free_port(), PT, full, out), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        assert np.array_equal(np.load(out % r), full)
+
+
+def test_assign_aggregates_partition_and_balance():
+    from ge_amd.dist import aggregate_cost, assign_aggregates
+    rs = np.random.RandomState(0)
+    sizes = np.concatenate([rs.randint(1, 60, 5000), rs.randint(2000, 12000, 50)])
+    pip = np.concatenate([[0], np.cumsum(sizes)])
+    cost = aggregate_cost(pip)
+    for world in (1, 2, 4, 8):
+        owned, loads = assign_aggregates(cost, world)
+        ids = np.sort(np.concatenate(owned))
+        assert np.array_equal(ids, np.arange(len(sizes)))  # every aggregate exactly once
+        assert all(np.all(np.diff(o) > 0) for o in owned)
+        assert max(loads) <= cost.sum() / world + cost.max()  # LPT bound
+        again, _ = assign_aggregates(cost, world)
+        assert all(np.array_equal(a, b) for a, b in zip(owned, again))

@@ -287,3 +287,33 @@ def test_faml_plan_device_resident_and_ranges(ctx, oracle):
             ctx.sync()
             plan.close()
         assert np.array_equal(X.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_faml_plan_aggregate_subsets_compose(ctx, oracle, world):
+    """ge_faml_plan_create_subset with the multi-GPU assignment (LPT by cost),
+    the ranks' plans run one after another on this GPU: together bit-exact."""
+    torch = pytest.importorskip("torch")
+    from ge_amd.dist import aggregate_cost, assign_aggregates
+    A = G.with_hubs(G.largest_component(G.rmat(6000, 50000, seed=5)), [(0, 2500)], seed=1)
+    n = len(A[0]) - 1
+    PT = oracle.partition(A, 0.125)[0]
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = G.random_coords(m, 3, seed=6)
+    rA = np.random.RandomState(7).uniform(0.05, 0.3, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=12, seed=9)
+    owned, _ = assign_aggregates(aggregate_cost(PT[0], A[0], PT[1]), world)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d = [T(A[0]), T(A[1]), T(A[2]), T(PT[0]), T(PT[1]), T(vA), T(cA), T(rA),
+         T(ge.uniform_stream(9, n * 3))]
+    ptr = [t.data_ptr() for t in d]
+    X = torch.zeros((n, 3), dtype=torch.float64, device=dev)
+    for aggs in owned:
+        plan = ge.FamlPlan(ctx, n, ptr[0], ptr[1], ptr[2], PT[0], ptr[3], ptr[4], ptr[5], 3,
+                           iterations=12, aggs=aggs)
+        plan.run(ptr[6], ptr[7], ptr[8], X.data_ptr())
+        ctx.sync()
+        plan.close()
+    assert np.array_equal(X.cpu().numpy(), want)
