@@ -27,9 +27,11 @@ def allgather_rows(x_full, chunk, rank, world):
     mine = x_full[rank * chunk:(rank + 1) * chunk].clone()
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(x_full, mine)
-    else:  # gloo: list form
-        parts = list(x_full.split(chunk))
-        dist.all_gather(parts, mine)
+    else:  # gloo: list form, staged through host memory for device tensors
+        host = x_full.cpu() if x_full.is_cuda else x_full
+        dist.all_gather(list(host.split(chunk)), mine.cpu())
+        if x_full.is_cuda:
+            x_full.copy_(host)
 
 
 class ShardedForceAtlas:
@@ -116,8 +118,10 @@ def allgather_members(X, rows_per_rank, rank, world):
     recv = torch.empty((world * width, X.shape[1]), dtype=X.dtype, device=dev)
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(recv, send)
-    else:
-        dist.all_gather(list(recv.split(width)), send)
+    else:  # gloo, staged through host memory for device tensors
+        host = recv.cpu()
+        dist.all_gather(list(host.split(width)), send.cpu())
+        recv.copy_(host)
     for r in range(world):
         if r != rank and counts[r]:
             X.index_copy_(0, idx[r], recv[r * width:r * width + counts[r]])
