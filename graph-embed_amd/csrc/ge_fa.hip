@@ -69,22 +69,26 @@ __global__ void degp1_kernel(int n, const int* __restrict__ ip, const double* __
 // skips the slots it has no rows in (wave-uniform), so the work per SIMD is
 // balanced to one 64-row slot.  The j range is streamed through an LDS tile of
 // 256 records {x_0..x_{D-1}, deg+1}; every row's sum runs over j ascending.
+// Independent work per lane for latency hiding comes from R rows and U
+// consecutive partners: the U*R pair terms are evaluated together and then
+// added to each row's sum in j order (R*U = 8; few rows per CU, as on a row
+// shard of N GPUs, take small R and large U).
 
 constexpr int kRepThreads = 512;
 constexpr int kTileJ = 256;
-constexpr int kRepR = 8;  // row slots per thread and chunk
+constexpr int kRepRU = 8;  // row slots x partners in flight per lane
 
 template <int D>
 struct Rec {
   static constexpr int W = (D + 1 <= 4) ? 4 : 8;  // doubles per LDS record
 };
 
-template <int D, bool REPEL_ONE>
+template <int D, bool REPEL_ONE, int R>
 __global__ void __launch_bounds__(kRepThreads)
 fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict__ X,
                   const double* __restrict__ dp1, double repel, double* __restrict__ Frep) {
   constexpr int W = Rec<D>::W;
-  constexpr int R = kRepR;
+  constexpr int U = kRepRU / R;
   __shared__ __attribute__((aligned(16))) double tile[kTileJ * W];
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
@@ -129,7 +133,31 @@ fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict
       // block-uniform: every coordinate of this tile and of the block's rows is
       // in the exact shared-reciprocal domain (ge_math.hpp)
       if (__syncthreads_and(ok)) {
-        for (int jj = 0; jj < cnt; ++jj) {
+        int jj = 0;
+        if (U > 1) {
+          for (; jj + U <= cnt; jj += U) {
+            double t[U][R][D];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const double* xj = &tile[(jj + u) * W];
+              const double dj = tile[(jj + u) * W + D];
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
+                if (r < nr) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
+              }
+            }
+            // in j order; a term alone is 0 + t (sum never -0, see ge_rows.hpp)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
+          }
+        }
+        for (; jj < cnt; ++jj) {
           const double* xj = &tile[jj * W];
           const double dj = tile[jj * W + D];
 #pragma unroll
@@ -602,12 +630,29 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
   int per = (rows + blocks - 1) / blocks;
   per = (per + 63) / 64 * 64;
   const int nb = (rows + per - 1) / per;
-  if (repel == 1.0)
-    hipLaunchKernelGGL((fa_repulse_strict<D, true>), dim3(nb), dim3(kRepThreads), 0, s, n, rb, re,
-                       per, X, dp1, repel, Frep);
-  else
-    hipLaunchKernelGGL((fa_repulse_strict<D, false>), dim3(nb), dim3(kRepThreads), 0, s, n, rb,
-                       re, per, X, dp1, repel, Frep);
+  // Row slots per lane.  Measured at C2 size (scripts/shard_tune.py): with
+  // more than 1024 rows per block 8 slots x 1 partner is fastest; below that
+  // 1 slot x 8 partners (R = 8 at 125 K rows: 379 Gpairs/s, R = 1: 469).
+  int R = per > 2 * kRepThreads ? 8 : 1;
+  if (const char* e = std::getenv("GE_REP_R")) {  // tuning / test override
+    const int r = std::atoi(e);
+    if (r == 1 || r == 2 || r == 4 || r == 8) R = r;
+  }
+  auto go = [&](auto RR) {
+    constexpr int RC = decltype(RR)::value;
+    if (repel == 1.0)
+      hipLaunchKernelGGL((fa_repulse_strict<D, true, RC>), dim3(nb), dim3(kRepThreads), 0, s, n,
+                         rb, re, per, X, dp1, repel, Frep);
+    else
+      hipLaunchKernelGGL((fa_repulse_strict<D, false, RC>), dim3(nb), dim3(kRepThreads), 0, s, n,
+                         rb, re, per, X, dp1, repel, Frep);
+  };
+  switch (R) {
+    case 8: go(std::integral_constant<int, 8>()); break;
+    case 4: go(std::integral_constant<int, 4>()); break;
+    case 2: go(std::integral_constant<int, 2>()); break;
+    default: go(std::integral_constant<int, 1>()); break;
+  }
 }
 
 template <int D>

@@ -75,6 +75,18 @@ def test_fa_degree_classes(ctx, oracle, use_weights):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("R", ["1", "2", "4", "8"])
+def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
+    """fa_repulse_strict with R row slots x 8/R partners in flight per lane
+    (row shards of N GPUs pick small R), ragged tiles and slot counts."""
+    monkeypatch.setenv("GE_REP_R", R)
+    A = G.rmat(9000, 60000, seed=3)
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=8)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=3)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3), want)
+
+
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
     # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
