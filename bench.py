@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--ml-iterations", type=int, default=100)
     ap.add_argument("--sweep-slots", action="store_true",
-                    help="c3: also time the streamed path at 1, 2 and 4 row slots per lane")
+                    help="c3: also time the streamed path's row-slot / partner variants")
     ap.add_argument("--end-to-end", action="store_true",
                     help="c3: also time partition::embed over the whole hierarchy")
     return ap.parse_args()
@@ -279,8 +279,10 @@ def run_c3(args, rank, world, local, dev):
         result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
     plan.close()
     if args.sweep_slots:  # streamed-path row slots per lane (tuning aid, stderr only)
-        for R in (1, 2, 4):
+        for R, U, B in ((1, 1, 8), (1, 1, 5), (1, 1, 4), (1, 1, 3), (1, 2, 4), (2, 1, 4)):
             os.environ["GE_FAML_R"] = str(R)
+            os.environ["GE_FAML_U"] = str(U)
+            os.environ["GE_FAML_BLOCKS_PER_CU"] = str(B)
             p2 = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
                              PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
                              args.dim, iterations=args.ml_iterations)
@@ -289,9 +291,12 @@ def run_c3(args, rank, world, local, dev):
             t0 = time.perf_counter()
             p2.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
             torch.cuda.synchronize(dev)
-            log(rank, f"sweep R={R}: {1e3 * (time.perf_counter() - t0):.1f} ms per call")
+            log(rank, f"sweep R={R} U={U} blocks/CU={B}: "
+                      f"{1e3 * (time.perf_counter() - t0):.1f} ms per call")
             p2.close()
         os.environ.pop("GE_FAML_R")
+        os.environ.pop("GE_FAML_U")
+        os.environ.pop("GE_FAML_BLOCKS_PER_CU")
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

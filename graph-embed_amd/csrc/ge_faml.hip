@@ -313,6 +313,7 @@ faml_resident(const int* __restrict__ order, const int* __restrict__ pack_beg,
 
 constexpr int kHT = 256;   // threads per block of the streamed kernels
 constexpr int kBigW = 64;  // records per wave tile
+constexpr int kBigDefaultR = 1, kBigDefaultU = 1;
 
 template <int D>
 __global__ void __launch_bounds__(kHT)
@@ -333,7 +334,9 @@ faml_huge_init(int nrows, const int* __restrict__ rows, const int* __restrict__ 
   DP[c] = internal_dp1(v, vA[v], ip, ix, dx, vA, use_weights);
 }
 
-template <int D, int R>
+// R row slots per lane, U consecutive partners evaluated together (their terms
+// are then added in j order).
+template <int D, int R, int U>
 __global__ void __launch_bounds__(kHT)
 faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ Xp,
@@ -386,7 +389,29 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
       }
       wave_lds_sync();
       if (__all(ok)) {
-        for (int jj = 0; jj < cnt; ++jj) {
+        int jj = 0;
+        if (U > 1) {
+          for (; jj + U <= cnt; jj += U) {
+            double t[U][R][D];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
+                if (r < nr)
+                  rep_pair<D, true, false>(xi[r], &tile[(jj + u) * WV], di[r],
+                                           tile[(jj + u) * WV + D], repel, t[u][r]);
+              }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
+          }
+        }
+        for (; jj < cnt; ++jj) {
           const double* xj = &tile[jj * WV];
           const double dj = tile[jj * WV + D];
 #pragma unroll
@@ -566,33 +591,40 @@ void build_packs(const std::vector<int>& ids, const int* h_pt_ip, int cap, int m
   if (cnt > 0) beg.push_back((int)order.size());
 }
 
+// Streamed repulsion variants: row slots R x partners in flight U.
+#define GE_BIG_VARIANTS(X) X(1, 1) X(1, 2) X(1, 4) X(2, 1) X(4, 1)
+constexpr int big_code(int R, int U) { return R * 8 + U; }
+
 template <int D>
-void launch_big_repulse(int R, int blocks, hipStream_t st, int nitems, const int2* items,
+void launch_big_repulse(int code, int blocks, hipStream_t st, int nitems, const int2* items,
                         int* queue, const int* pt_ip, const double* X, const double* DP,
                         double repel, double* F) {
-  switch (R) {
-    case 4:
-      hipLaunchKernelGGL((faml_big_repulse<D, 4>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
-                         queue, pt_ip, X, DP, repel, F);
-      break;
-    case 2:
-      hipLaunchKernelGGL((faml_big_repulse<D, 2>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
-                         queue, pt_ip, X, DP, repel, F);
-      break;
+  switch (code) {
+#define GE_BIG_LAUNCH(RR, UU)                                                                 \
+  case big_code(RR, UU):                                                                      \
+    hipLaunchKernelGGL((faml_big_repulse<D, RR, UU>), dim3(blocks), dim3(kHT), 0, st, nitems, \
+                       items, queue, pt_ip, X, DP, repel, F);                                 \
+    break;
+    GE_BIG_VARIANTS(GE_BIG_LAUNCH)
+#undef GE_BIG_LAUNCH
     default:
-      hipLaunchKernelGGL((faml_big_repulse<D, 1>), dim3(blocks), dim3(kHT), 0, st, nitems, items,
-                         queue, pt_ip, X, DP, repel, F);
+      throw Error(GE_ERR_STATE, "unknown streamed repulsion variant");
   }
 }
 
-// resident blocks per CU of faml_big_repulse<dim, R>
-int rep_occupancy(int dim, int R) {
+// resident blocks per CU of faml_big_repulse<dim, R, U>
+int rep_occupancy(int dim, int code) {
   int nb = 1;
   dispatch_dim(dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    const void* k = R == 4   ? (const void*)faml_big_repulse<D, 4>
-                    : R == 2 ? (const void*)faml_big_repulse<D, 2>
-                             : (const void*)faml_big_repulse<D, 1>;
+    const void* k = nullptr;
+    switch (code) {
+#define GE_BIG_KERNEL(RR, UU) \
+  case big_code(RR, UU): k = (const void*)faml_big_repulse<D, RR, UU>; break;
+      GE_BIG_VARIANTS(GE_BIG_KERNEL)
+#undef GE_BIG_KERNEL
+      default: k = (const void*)faml_big_repulse<D, 1, 1>;
+    }
     GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kHT, 0));
   });
   return std::max(nb, 1);
@@ -616,7 +648,7 @@ struct ge_faml_plan {
   ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge;
   ge::RowClasses ecls;
   ge::DevBuf<int2> items;
-  int nrows = 0, nitems = 0, R = 1, rep_blocks = 0;
+  int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
   double streamed_pairs = 0.0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
   // the size classes are independent: streamed path, large, mid and small
@@ -679,15 +711,18 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   std::vector<int> rows;
   for (int a : big)
     for (int li = 0; li < h_pt_ip[a + 1] - h_pt_ip[a]; ++li) rows.push_back(h_pt_ip[a] + li);
-  int R = 0;
+  // row slots x partners in flight (GE_FAML_R / GE_FAML_U override; only the
+  // compiled variants of GE_BIG_VARIANTS are accepted)
+  int R = kBigDefaultR, U = kBigDefaultU;
   if (const char* e = std::getenv("GE_FAML_R")) R = std::atoi(e);
-  if (R != 1 && R != 2 && R != 4) {
-    // enough items for ~2 per wave slot at the occupancy of the R variant
-    R = 1;
-    for (int r : {4, 2}) {
-      const double slots = (double)cus * rep_occupancy(dim, r) * (kHT / 64);
-      if ((double)rows.size() / (64.0 * r) >= 2.0 * slots) { R = r; break; }
-    }
+  if (const char* e = std::getenv("GE_FAML_U")) U = std::atoi(e);
+  bool known = false;
+#define GE_BIG_KNOWN(RR, UU) known = known || (R == RR && U == UU);
+  GE_BIG_VARIANTS(GE_BIG_KNOWN)
+#undef GE_BIG_KNOWN
+  if (!known) {
+    R = kBigDefaultR;
+    U = kBigDefaultU;
   }
   std::vector<int> erows;
   if (!rows.empty()) {  // degree classes of the streamed members' CSR rows
@@ -718,11 +753,17 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   std::vector<int2> items;
   for (const Item& it : its) items.push_back(make_int2(it.a, it.r0));
   pl->R = R;
+  pl->code = big_code(R, U);
   for (int a : big) {
     const double sa = h_pt_ip[a + 1] - h_pt_ip[a];
     pl->streamed_pairs += sa * (sa - 1);
   }
-  pl->rep_blocks = cus * rep_occupancy(dim, R);
+  // 4 waves per SIMD: more items per wave for the queue to balance (C3 level
+  // 0: 961 ms per call against 1091 ms at the full 8 waves per SIMD)
+  int blocks_cu = std::min(4, rep_occupancy(dim, pl->code));
+  if (const char* e = std::getenv("GE_FAML_BLOCKS_PER_CU"))  // tuning override
+    blocks_cu = std::max(1, std::min(blocks_cu, std::atoi(e)));
+  pl->rep_blocks = cus * blocks_cu;
   std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
   pl->off_m = begs.size();
@@ -812,7 +853,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_rev += 2;
           GE_HIP(hipEventRecord(re[0], ss));
         }
-        launch_big_repulse<D>(pl->R, pl->rep_blocks, ss, pl->nitems, pl->items.p,
+        launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                               pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
         if (re) GE_HIP(hipEventRecord(re[1], ss));
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx,

@@ -195,11 +195,12 @@ def test_faml_size_classes(ctx, oracle, sizes):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("R", [1, 2, 4])
-def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R):
+@pytest.mark.parametrize("R,U", [(1, 1), (1, 2), (1, 4), (2, 1), (4, 1)])
+def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U):
     """Streamed path (faml_big_repulse / faml_big_edges) with 1, 2 and 4 row
     slots per lane, ragged last items, and hub rows longer than one 64-edge chunk."""
     monkeypatch.setenv("GE_FAML_R", str(R))
+    monkeypatch.setenv("GE_FAML_U", str(U))
     sizes = [3000, 700, 2203, 90, 1]
     n = sum(sizes)
     A = G.with_hubs(G.rmat(n, 10 * n, seed=7), [(3, 2600), (40, 5000)], seed=R)
