@@ -442,9 +442,31 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
 // Per streamed member, after faml_big_repulse: the CSR row (:415-467) added to
 // the repulsion sum in stored order (degree-classed, ge_rows.hpp), gravity
 // (:469-474) and the swing/speed update (:477-530).
+// ecode[e] for a streamed member's CSR entry e: the neighbour's P_T position
+// when the entry is internal (v_A[j] == a && j != local i, :417), else
+// -(v_A[j] + 1).  Static per level, so the per-iteration edge pass does one
+// gather per entry instead of three dependent ones.
+__global__ void edge_code_kernel(int nrows, const int* __restrict__ rows,
+                                 const int* __restrict__ pt_ip, const int* __restrict__ pt_ix,
+                                 const int* __restrict__ pos_of, const int* __restrict__ vA,
+                                 const int* __restrict__ ip, const int* __restrict__ ix,
+                                 int* __restrict__ ecode) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nrows) return;
+  const int c = rows[q];
+  const int v = pt_ix[c];
+  const int a = vA[v];
+  const int li = c - pt_ip[a];
+  for (int e = ip[v]; e < ip[v + 1]; ++e) {
+    const int j = ix[e];
+    const int b = vA[j];
+    ecode[e] = (b == a && j != li) ? pos_of[j] : -(b + 1);
+  }
+}
+
 template <int D>
 struct FamlRows {
-  const int *pt_ip, *pt_ix, *pos_of, *vA, *ip, *ix;
+  const int *pt_ip, *pt_ix, *ecode, *ip, *vA;
   const double *dx, *cA, *Xc, *DP, *Fscr;
   double *Xn, *Fprev;
   MlConst c;
@@ -477,10 +499,9 @@ struct FamlRows {
     s.ca_ok = all_coord_ok<D>(cA + (size_t)s.a * D);
   }
   __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
-    const int j = ix[e];
-    const int b = vA[j];
-    if (b == s.a && j != s.li) {  // sic: global j against local i (:417)
-      const double* xj = Xc + (size_t)pos_of[j] * D;
+    const int code = ecode[e];
+    if (code >= 0) {  // internal entry (edge_code_kernel)
+      const double* xj = Xc + (size_t)code * D;
       const double wt = c.use_weights ? dx[e] : 1.0;
       if (s.row_ok && all_coord_ok<D>(xj))
         attr_edge<D, true>(s.xi, xj, wt, s.dip1, c, t);
@@ -488,7 +509,7 @@ struct FamlRows {
         attr_edge<D, false>(s.xi, xj, wt, s.dip1, c, t);
     } else {
       const double* ca = cA + (size_t)s.a * D;
-      const double* cb = cA + (size_t)b * D;
+      const double* cb = cA + (size_t)(-code - 1) * D;
       if (s.row_ok && s.ca_ok && all_coord_ok<D>(cb))
         pull_edge<D, true>(ca, cb, s.mag, s.rmag, t);
       else
@@ -645,7 +666,7 @@ struct ge_faml_plan {
   ge::FaConst c{};
   int ns = 0, nm = 0, nl = 0, nhuge = 0;
   size_t off_m = 0, off_l = 0;
-  ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge;
+  ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge, ecode;
   ge::RowClasses ecls;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
@@ -737,6 +758,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       deg[q] = h_ip[v + 1] - h_ip[v];
     }
     classify_rows(rows, deg, erows, pl->ecls.nheavy, pl->ecls.nmed, pl->ecls.nlight);
+    pl->ecode.alloc(std::max(h_ip[pl->n], 1));
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
     pl->ecls.rows = pl->erows.p;
@@ -799,6 +821,10 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   }
   hipLaunchKernelGGL(pos_of_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, pl->pt_ix,
                      pl->pos.p);
+  if (pl->nrows > 0)
+    hipLaunchKernelGGL(edge_code_kernel, dim3((pl->nrows + 255) / 256), dim3(256), 0, st,
+                       pl->nrows, pl->rows.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip,
+                       pl->ix, pl->ecode.p);
   GE_HIP(hipGetLastError());
   for (int k = 0; k < 3; ++k) {
     GE_HIP(hipStreamCreateWithFlags(&pl->side[k], hipStreamNonBlocking));
@@ -856,7 +882,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
         launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                               pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
         if (re) GE_HIP(hipEventRecord(re[1], ss));
-        const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx,
+        const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
                              cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
         hipLaunchKernelGGL((classed_rows_kernel<D, FamlRows<D>>), dim3(pl->ecls.grid()),
                            dim3(kRowT), 0, ss, pl->ecls, fr);

@@ -21,6 +21,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <vector>
 
 namespace ge {
@@ -37,17 +38,21 @@ struct RowClasses {
 };
 
 // Host: order `ids` (row ids with their degrees) into heavy, medium, light.
+// GE_ROWS_MED / GE_ROWS_HEAVY override the class bounds (tuning only).
 inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
                           std::vector<int>& out, int& nheavy, int& nmed, int& nlight) {
+  int med = kMedDeg, heavy = kHeavyDeg;
+  if (const char* e = std::getenv("GE_ROWS_MED")) med = std::atoi(e);
+  if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::atoi(e);
   out.clear();
   for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] > kHeavyDeg) out.push_back(ids[q]);
+    if (deg[q] > heavy) out.push_back(ids[q]);
   nheavy = (int)out.size();
   for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] > kMedDeg && deg[q] <= kHeavyDeg) out.push_back(ids[q]);
+    if (deg[q] > med && deg[q] <= heavy) out.push_back(ids[q]);
   nmed = (int)out.size() - nheavy;
   for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] <= kMedDeg) out.push_back(ids[q]);
+    if (deg[q] <= med && deg[q] <= heavy) out.push_back(ids[q]);
   nlight = (int)out.size() - nheavy - nmed;
 }
 
@@ -66,12 +71,16 @@ __device__ __forceinline__ void group_sync() {
 }
 
 // acc += term(e0) + term(e0+1) + ... in order; G threads (g = 0..G-1) share buf
-// (G*U*D doubles).  Every thread of the group ends with the same acc.
+// (G*U*D doubles, 16-byte aligned).  The terms are evaluated by all G threads;
+// the ordered adds are done by the group's first wave only (for G = 64: the
+// whole group), whose lanes all end with the same acc -- the other waves'
+// acc is not updated.  Two terms (2D doubles) are read with D 16-byte loads.
 template <int D, int G, int U, class Term>
 __device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* buf, Term&& term,
                                                  double (&acc)[D]) {
+  const bool summer = G == 64 || g < 64;
   for (int b = e0; b < e1; b += G * U) {
-    group_sync<G>();  // the previous chunk has been read by everyone
+    group_sync<G>();  // the previous chunk has been read
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = b + g + G * u;
@@ -85,11 +94,28 @@ __device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* 
       }
     }
     group_sync<G>();
-    const int cnt = min(G * U, e1 - b);
-#pragma unroll 4
-    for (int l = 0; l < cnt; ++l)
+    if (summer) {
+      const int cnt = min(G * U, e1 - b);
+      int l = 0;
+#pragma unroll 2
+      for (; l + 1 < cnt; l += 2) {
+        const double2* p = reinterpret_cast<const double2*>(buf + l * D);  // l even: aligned
+        double v[2 * D];
 #pragma unroll
-      for (int k = 0; k < D; ++k) acc[k] = acc[k] + buf[l * D + k];
+        for (int q = 0; q < D; ++q) {
+          const double2 w = p[q];
+          v[2 * q] = w.x;
+          v[2 * q + 1] = w.y;
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[k];
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[D + k];
+      }
+      if (l < cnt)
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + buf[l * D + k];
+    }
   }
 }
 
@@ -98,7 +124,7 @@ __device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* 
 //   load(row, State&), term(const State&, e, t[D]), finish(State&, bool writer).
 template <int D, class P>
 __global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) {
-  __shared__ double buf[kRowT * kHeavyU * D];
+  __shared__ __attribute__((aligned(16))) double buf[kRowT * kHeavyU * D];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   typename P::State st;
