@@ -40,120 +40,129 @@
 namespace ge {
 namespace {
 
-// Open-addressing int -> double map (linear probing, tombstones).
+// int -> double map: entries kept dense (keys_/vals_, iteration touches live
+// entries only), located through an open-addressing index table (linear
+// probing, tombstones).  Erase moves the last entry into the hole.
 class NbrMap {
  public:
   static constexpr int kEmpty = -1, kTomb = -2;
-  int size() const { return live_; }
+  int size() const { return (int)keys_.size(); }
 
   void reserve(int want) {
+    keys_.reserve(want);
+    vals_.reserve(want);
     int cap = 4;
     while (cap < 2 * want) cap <<= 1;
-    if (cap > (int)keys_.size()) rehash(cap);
+    if (cap > (int)table_.size()) rehash(cap);
   }
   // first insertion wins (std::map::insert semantics)
   void insert_new(int k, double v) {
     grow_if_needed();
-    int at = probe(k);
-    if (keys_[at] == k) return;
+    const int at = probe(k);
+    if (table_[at] >= 0) return;
     place(at, k, v);
   }
   // m[k] += v (operator[] then +=: 0.0 + v for a new key)
   void add(int k, double v) {
     grow_if_needed();
-    int at = probe(k);
-    if (keys_[at] == k) {
-      vals_[at] += v;
+    const int at = probe(k);
+    if (table_[at] >= 0) {
+      vals_[table_[at]] += v;
       return;
     }
     place(at, k, 0.0 + v);
   }
   const double* find(int k) const {
-    if (keys_.empty()) return nullptr;
-    const int mask = (int)keys_.size() - 1;
-    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
-      if (keys_[h] == k) return &vals_[h];
-      if (keys_[h] == kEmpty) return nullptr;
-    }
+    const int at = locate(k);
+    return at < 0 ? nullptr : &vals_[table_[at]];
   }
   void erase(int k) {
-    if (keys_.empty()) return;
-    const int mask = (int)keys_.size() - 1;
-    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
-      if (keys_[h] == k) {
-        keys_[h] = kTomb;
-        --live_;
-        return;
-      }
-      if (keys_[h] == kEmpty) return;
+    const int at = locate(k);
+    if (at < 0) return;
+    const int idx = table_[at];
+    table_[at] = kTomb;
+    const int last = (int)keys_.size() - 1;
+    if (idx != last) {
+      table_[locate(keys_[last])] = idx;
+      keys_[idx] = keys_[last];
+      vals_[idx] = vals_[last];
     }
+    keys_.pop_back();
+    vals_.pop_back();
   }
-  int capacity() const { return (int)keys_.size(); }
-  // visit slots [b, e) (for splitting one large map across threads)
+  // visit entries [b, e) of the dense order (for splitting one map across threads)
   template <class F>
   void for_range(int b, int e, F&& f) const {
-    for (int h = b; h < e; ++h)
-      if (keys_[h] >= 0) f(keys_[h], vals_[h]);
+    for (int x = b; x < e; ++x) f(keys_[x], vals_[x]);
   }
   template <class F>
   void for_each(F&& f) const {
-    for (size_t h = 0; h < keys_.size(); ++h)
-      if (keys_[h] >= 0) f(keys_[h], vals_[h]);
+    for (size_t x = 0; x < keys_.size(); ++x) f(keys_[x], vals_[x]);
   }
   void clear() {
     std::vector<int>().swap(keys_);
     std::vector<double>().swap(vals_);
-    live_ = used_ = 0;
+    std::vector<int>().swap(table_);
+    used_ = 0;
   }
 
  private:
   static int hash(int k) { return (int)(((uint32_t)k * 2654435761u) >> 1); }
+  // table slot holding k, or -1
+  int locate(int k) const {
+    if (table_.empty()) return -1;
+    const int mask = (int)table_.size() - 1;
+    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
+      const int t = table_[h];
+      if (t == kEmpty) return -1;
+      if (t >= 0 && keys_[t] == k) return h;
+    }
+  }
   // slot of k if present, else the first free slot (tombstone or empty) on its chain
   int probe(int k) const {
-    const int mask = (int)keys_.size() - 1;
+    const int mask = (int)table_.size() - 1;
     int tomb = -1;
     for (int h = hash(k) & mask;; h = (h + 1) & mask) {
-      if (keys_[h] == k) return h;
-      if (keys_[h] == kTomb) {
+      const int t = table_[h];
+      if (t >= 0) {
+        if (keys_[t] == k) return h;
+      } else if (t == kTomb) {
         if (tomb < 0) tomb = h;
-      } else if (keys_[h] == kEmpty) {
+      } else {
         return tomb >= 0 ? tomb : h;
       }
     }
   }
   void place(int at, int k, double v) {
-    if (keys_[at] == kEmpty) ++used_;
-    keys_[at] = k;
-    vals_[at] = v;
-    ++live_;
+    if (table_[at] == kEmpty) ++used_;
+    table_[at] = (int)keys_.size();
+    keys_.push_back(k);
+    vals_.push_back(v);
   }
   void grow_if_needed() {
-    if (keys_.empty()) {
+    if (table_.empty()) {
       rehash(4);
-    } else if (2 * (used_ + 1) > (int)keys_.size()) {
-      int cap = (int)keys_.size();
-      while (4 * (live_ + 1) > cap) cap <<= 1;  // keep load <= 1/4 after rehash
-      rehash(std::max(cap, 4));
+    } else if (2 * (used_ + 1) > (int)table_.size()) {
+      int cap = 4;
+      while (cap < 4 * ((int)keys_.size() + 1)) cap <<= 1;  // load <= 1/4 after rehash
+      rehash(cap);
     }
   }
   void rehash(int cap) {
-    std::vector<int> ok(cap, kEmpty);
-    std::vector<double> ov(cap);
+    std::vector<int> t(cap, kEmpty);
     const int mask = cap - 1;
-    for (size_t h = 0; h < keys_.size(); ++h) {
-      if (keys_[h] < 0) continue;
-      int at = hash(keys_[h]) & mask;
-      while (ok[at] != kEmpty) at = (at + 1) & mask;
-      ok[at] = keys_[h];
-      ov[at] = vals_[h];
+    for (size_t x = 0; x < keys_.size(); ++x) {
+      int at = hash(keys_[x]) & mask;
+      while (t[at] != kEmpty) at = (at + 1) & mask;
+      t[at] = (int)x;
     }
-    keys_.swap(ok);
-    vals_.swap(ov);
-    used_ = live_;
+    table_.swap(t);
+    used_ = (int)keys_.size();
   }
   std::vector<int> keys_;
   std::vector<double> vals_;
-  int live_ = 0, used_ = 0;
+  std::vector<int> table_;
+  int used_ = 0;  // table slots not kEmpty
 };
 
 struct Bitmap {
@@ -208,7 +217,9 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   std::vector<int> arg(n, 0);
   // runner-up of each clean vertex's last scan (value, index) under the same
   // order (eta descending, index ascending).  Etas only fall while a vertex stays
-  // clean, so it is an upper bound on the current runner-up.
+  // clean, so it is an upper bound on the current runner-up.  second_idx = -1:
+  // the scan found no runner-up; kUnknown: not known (after a demotion).
+  constexpr int kUnknown = -2;
   std::vector<double> second(n, -inf);
   std::vector<int> second_idx(n, -1);
   std::vector<int> work(n);  // dirty vertices
@@ -242,20 +253,63 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   // v became busy: a clean watcher k whose only candidate was v (no runner-up)
   // now has none -- exactly what its rescan would find -- and gets v back at
   // the end of the round if v survives; the others rescan.
-  std::vector<std::pair<int, int>> lost;
+  std::vector<std::pair<int, int>> lost, pending, demoted;
+  long long ustat = 0;
   auto consume_busy = [&](int v) {
     for (int k : watch[v]) {
       if (arg[k] != v || dirty[k]) continue;
-      if (second_idx[k] < 0) {
+      if (second_idx[k] == -1) {
         best[k] = -inf;
         arg[k] = -1;
         set_cand(k);
         lost.emplace_back(k, v);
+      } else if (second_idx[k] >= 0) {
+        pending.emplace_back(k, v);  // demoted to its runner-up after this resolve
       } else {
+        ++ustat;
         mark(k);
       }
     }
     std::vector<int>().swap(watch[v]);
+  };
+  auto eta_of = [&](int k, int j, double& eta) {
+    const double* w = adj[k].find(j);
+    if (!w) return false;
+    eta = 2 * (*w / T - alpha[k] * alpha[j]);
+    return true;
+  };
+  // After a resolve: a clean k whose max v became busy.  The reference rescans
+  // k in the next pass and finds the best non-busy neighbour.  If k's recorded
+  // runner-up s is not busy and its eta is unchanged, s is that neighbour: every
+  // other candidate was <= it at k's last scan and etas only fell since.  The
+  // runner-up behind s is then unknown.  (k, v) is remembered so that v, free
+  // again at the end of the round, can be compared back in without a rescan.
+  long long pstat[5] = {0, 0, 0, 0, 0};
+  auto apply_pending = [&]() {
+    for (const auto& kv : pending) {
+      const int k = kv.first, v = kv.second;
+      if (dirty[k] || dead[k] || arg[k] != v) continue;
+      const int sidx = second_idx[k];
+      double eta;
+      if (prof) {
+        if (sidx < 0) ++pstat[0];
+        else if (busy[sidx]) ++pstat[1];
+        else if (dead[sidx]) ++pstat[2];
+        else if (!eta_of(k, sidx, eta) || eta != second[k]) ++pstat[3];
+        else ++pstat[4];
+      }
+      if (sidx >= 0 && !busy[sidx] && !dead[sidx] && eta_of(k, sidx, eta) && eta == second[k]) {
+        best[k] = eta;
+        arg[k] = sidx;
+        second_idx[k] = kUnknown;
+        set_cand(k);
+        watch[sidx].push_back(k);
+        demoted.emplace_back(k, v);
+      } else {
+        mark(k);
+      }
+    }
+    pending.clear();
   };
   // keep's alpha grew: a clean watcher k keeps keep as its max if the new eta
   // still beats the (upper bound of the) runner-up; then only max_eta changes.
@@ -264,6 +318,10 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     stay.clear();
     for (int k : watch[v]) {
       if (arg[k] != v || dirty[k]) continue;
+      if (second_idx[k] == kUnknown) {
+        mark(k);
+        continue;
+      }
       const double* w = adj[k].find(v);
       bool kept = false;
       if (w) {
@@ -311,7 +369,8 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   };
 
   double t_scan = 0, t_resolve = 0, t_merge = 0, t_pop = 0, t_cls = 0, t_par = 0;
-  long long rescans = 0;
+  double t_snap = 0, t_swap = 0, t_lost = 0;
+  long long rescans = 0, slots_scanned = 0, slots_big = 0, live_scanned = 0;
   int rounds = 0;
   std::vector<int> todo, keep_dirty, late, big, small_todo;
   int M_prev = M;
@@ -371,18 +430,25 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       };
       big.clear();
       small_todo.clear();
-      for (int x = 0; x < nt; ++x)
-        (adj[todo[x]].capacity() > 8192 ? big : small_todo).push_back(todo[x]);
+      for (int x = 0; x < nt; ++x) {
+        const int cap = adj[todo[x]].size();
+        (cap > 4096 ? big : small_todo).push_back(todo[x]);
+        if (prof) {
+          slots_scanned += cap;
+          if (cap > 8192) slots_big += cap;
+          live_scanned += adj[todo[x]].size();
+        }
+      }
       const int nsm = (int)small_todo.size();
 #pragma omp parallel for schedule(dynamic, 64)
       for (int x = 0; x < nsm; ++x) {
         Top2 t;
         const int i = small_todo[x];
-        scan_range(i, 0, adj[i].capacity(), t);
+        scan_range(i, 0, adj[i].size(), t);
         store(i, t);
       }
       for (int i : big) {  // one large neighbourhood split across threads
-        const int cap = adj[i].capacity();
+        const int cap = adj[i].size();
         Top2 acc;
 #pragma omp parallel
         {
@@ -436,6 +502,7 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
           dQ += best[i];
         }
       }
+      apply_pending();
       t_resolve += secs(t1, now());
     }
     // ---- contraction (:1756-1779)
@@ -479,6 +546,8 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       basis = alive;
       N = M;
     }
+    const auto t4 = now();
+    t_snap += secs(t3, t4);
     // ---- swap-pop + union (:1819-1834); the candidate bit moves with its vertex
     for (const auto& mg : merges) {
       const int keep = mg.first, gone = mg.second;
@@ -497,6 +566,8 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       busy[keep] = 0;
       M -= 1;
     }
+    const auto t5 = now();
+    t_swap += secs(t4, t5);
     // single-candidate vertices that lost their partner to busy get it back
     // (it was scanned in pass 1, when nothing was busy, so v is its only
     // neighbour; any change to its adjacency would have marked it dirty)
@@ -514,6 +585,32 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       watch[v].push_back(k);
     }
     lost.clear();
+    const auto t6 = now();
+    t_lost += secs(t5, t6);
+    // demoted vertices: their old max v is free again (or dead, and then k's
+    // adjacency changed and k is dirty).  v comes back if it beats the current
+    // max under the scan order; the other candidates are <= the current max.
+    for (const auto& kv : demoted) {
+      const int k = kv.first, v = kv.second;
+      if (dirty[k] || dead[k] || dead[v] || arg[k] < 0 || busy[k]) continue;
+      double eta;
+      if (!eta_of(k, v, eta)) {
+        mark(k);
+        continue;
+      }
+      const int a = arg[k];
+      if (eta > best[k] || (eta == best[k] && v < a)) {
+        second[k] = best[k];
+        second_idx[k] = a;
+        best[k] = eta;
+        arg[k] = v;
+        watch[v].push_back(k);
+      } else {
+        second_idx[k] = kUnknown;
+      }
+      set_cand(k);
+    }
+    demoted.clear();
     t_pop += secs(t3, now());
     if (prof && std::getenv("GE_PROFILE_ROUNDS"))
       std::fprintf(stderr, "round %d alive %d merges %zu rescans_total %lld\n", rounds, M,
@@ -526,7 +623,14 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
                  "merge %.3fs snap+pop %.3fs\n",
                  n, rounds, secs(t_start, now()), t_scan, rescans, t_resolve, t_merge, t_pop);
   if (prof)
-    std::fprintf(stderr, "scan split: classify %.3fs parallel %.3fs\n", t_cls, t_par);
+    std::fprintf(stderr, "scan split: classify %.3fs parallel %.3fs; slots %lld (big maps %lld), live entries %lld\n",
+                 t_cls, t_par, slots_scanned, slots_big, live_scanned);
+  if (prof)
+    std::fprintf(stderr, "snap+pop split: snap %.3fs swap-pop %.3fs lost %.3fs demoted %.3fs\n",
+                 t_snap, t_swap, t_lost, t_pop - t_snap - t_swap - t_lost);
+  if (prof)
+    std::fprintf(stderr, "demotions: no-runner-up %lld runner-up busy %lld dead %lld changed %lld ok %lld; unknown->mark %lld\n",
+                 pstat[0], pstat[1], pstat[2], pstat[3], pstat[4], ustat);
   if (prof)
     std::fprintf(stderr, "marks: init %lld resolve %lld gone-nbrs %lld keep %lld late %lld\n",
                  msrc[0], msrc[1], msrc[2], msrc[3], msrc[4]);
