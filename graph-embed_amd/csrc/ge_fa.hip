@@ -369,6 +369,8 @@ struct FaRows {
 constexpr int kSmallMax = 512;  // one row group per thread group below
 constexpr int kSmallT = 512;
 constexpr int kSmallNnz = 6144;
+// CSR entries staged in LDS (the 4-D double-buffered term tile leaves less room)
+constexpr int small_nnz_cap(int D) { return D == 4 ? 4096 : kSmallNnz; }
 
 // The G lanes of a group hold U terms each (term u of lane g is partner
 // g + G*u of the chunk); the group's first lane adds the first cnt in order.
@@ -409,19 +411,62 @@ __device__ __forceinline__ void group_add(const double (&t)[U][D], int tid, int 
   wave_lds_sync();
 }
 
+// Software-pipelined ordered group sum for the domain-only kernel: the terms
+// of chunk c+1 are evaluated while the sums of chunk c are formed, in one
+// branch-free block (every lane of a group adds its group's terms; all end
+// with the same acc).  term(q, t) writes the term of chunk-local item q.
+// tb holds two chunk buffers of T*D doubles.
+template <int D, int G, int T, class Term>
+__device__ __forceinline__ void pipelined_group_sum(int nitems, int tid, int g, double* tb,
+                                                    Term&& term, double (&acc)[D]) {
+  if (nitems <= 0) return;
+  const int base = tid - g;
+  double t[D];
+  term(g, t);  // chunk 0
+#pragma unroll
+  for (int k = 0; k < D; ++k) tb[tid * D + k] = t[k];
+  for (int c0 = 0; c0 < nitems; c0 += G) {
+    const int cur = (c0 / G) & 1;
+    wave_lds_sync();
+    const bool more = c0 + G < nitems;
+    if (more) term(c0 + G + g, t);  // next chunk, independent of the adds below
+    const int cnt = min(G, nitems - c0);
+    const double* src = tb + cur * T * D + base * D;
+#pragma unroll
+    for (int l = 0; l < G; ++l)
+      if (l < cnt)
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + src[l * D + k];
+    wave_lds_sync();
+    if (more)
+#pragma unroll
+      for (int k = 0; k < D; ++k) tb[((cur ^ 1) * T + tid) * D + k] = t[k];
+  }
+}
+
 // STAGED: the CSR indices and weights (nnz <= kSmallNnz) are copied to LDS once.
-template <int D, int G, int U, bool STAGED>
-__global__ void __launch_bounds__(kSmallT)
+// DOMAIN_ONLY: the branch-free in-domain bodies only.  Such a kernel stops at
+// the first iteration whose rows leave the exact-division domain (or at
+// stop_at, a test hook) and records it in *it_state; the general kernel (both bodies) resumes from *it_state.
+// State crossing between the two: coordinates in Xg, previous forces in Fp.
+// Splitting keeps the fast kernel within 128 VGPRs, so it runs 1024 threads;
+// it has the linear attraction only and is skipped for linlog / delta != 1.
+template <int D, int G, int T, bool STAGED, bool DOMAIN_ONLY>
+__global__ void __launch_bounds__(T)
 fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
                 const double* __restrict__ dxg, const double* __restrict__ dp1g,
-                double* __restrict__ Xg, int iterations, FaConst c) {
+                double* __restrict__ Xg, double* __restrict__ Fp, int* __restrict__ it_state,
+                int iterations, int stop_at, FaConst c) {
   constexpr int W = Rec<D>::W;
+  constexpr int U = 1;
   __shared__ __attribute__((aligned(16))) double sx[kSmallMax * W];
-  __shared__ double tb[(G > 1 ? kSmallT * U : 1) * D];
-  __shared__ int s_ix[STAGED ? kSmallNnz : 1];
-  __shared__ double s_dx[STAGED ? kSmallNnz : 1];
+  __shared__ double tb[(G > 1 ? T * U * (DOMAIN_ONLY ? 2 : 1) : 1) * D];
+  __shared__ int s_ix[STAGED ? small_nnz_cap(D) : 1];
+  __shared__ double s_dx[STAGED ? small_nnz_cap(D) : 1];
+  const int it0 = DOMAIN_ONLY ? 0 : *it_state;
+  if (it0 >= iterations) return;
   if (STAGED) {
-    for (int e = threadIdx.x; e < ip[n]; e += kSmallT) {
+    for (int e = threadIdx.x; e < ip[n]; e += T) {
       s_ix[e] = ixg[e];
       s_dx[e] = dxg[e];
     }
@@ -433,7 +478,7 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
   const int i = tid / G;
   const bool active = i < n;
   const bool leader = active && g == 0;
-  for (int q = tid; q < n; q += kSmallT) {
+  for (int q = tid; q < n; q += T) {
 #pragma unroll
     for (int k = 0; k < D; ++k) sx[q * W + k] = Xg[(size_t)q * D + k];
     sx[q * W + D] = dp1g[q];
@@ -442,9 +487,12 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
   const int e1 = active ? ip[i + 1] : 0;
   double fprev[D], F[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) fprev[k] = F[k] = 0.0;
-
-  for (int it = 0; it < iterations; ++it) {
+  for (int k = 0; k < D; ++k) {
+    fprev[k] = leader ? Fp[(size_t)i * D + k] : 0.0;
+    F[k] = 0.0;
+  }
+  int it = it0;
+  for (; it < iterations; ++it) {
     __syncthreads();
     double xi[D], acc[D];
 #pragma unroll
@@ -456,8 +504,32 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
     const bool row_ok = all_coord_ok<D>(xi);
     const bool rep_ok = row_ok && weight_ok(dip1) && weight_ok(c.repel);
     // every row in the shared-reciprocal domain: branch-free pair and edge
-    // bodies the compiler can interleave across the U terms of a lane
-    if (__syncthreads_and(!active || rep_ok)) {
+    // bodies the compiler can interleave
+    const bool dom = __syncthreads_and(!active || rep_ok);
+    if (DOMAIN_ONLY && (!dom || it == stop_at)) break;  // block-uniform: hand over
+    if (DOMAIN_ONLY && G > 1) {
+      // :151-167, j ascending; then :169-203, CSR order
+      pipelined_group_sum<D, G, T>(n, tid, g, tb, [&](int q, double (&t)[D]) {
+        const int jj = min(q, n - 1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+        rep_pair<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t);
+        if (q >= n)
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[k] = 0.0;
+      }, acc);
+      pipelined_group_sum<D, G, T>(e1 - e0, tid, g, tb, [&](int q, double (&t)[D]) {
+        const int ee = min(e0 + q, e1 - 1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+        if (e1 > e0)
+          attr_edge<D, true, true>(xi, &sx[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, dip1, c,
+                                   t);
+        if (e0 + q >= e1)
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[k] = 0.0;
+      }, acc);
+    } else if (DOMAIN_ONLY || dom) {
       for (int j0 = 0; j0 < n; j0 += G * U) {  // :151-167, j ascending
         double t[U][D];
 #pragma unroll
@@ -481,49 +553,50 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
           const int ee = min(e, e1 - 1);
 #pragma unroll
           for (int k = 0; k < D; ++k) t[u][k] = 0.0;
-          attr_edge<D, true>(xi, &sx[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, dip1, c, t[u]);
+          attr_edge<D, true, DOMAIN_ONLY>(xi, &sx[ix[ee] * W], c.use_weights ? dx[ee] : 1.0,
+                                          dip1, c, t[u]);
           if (e >= e1)
 #pragma unroll
             for (int k = 0; k < D; ++k) t[u][k] = 0.0;
         }
         group_add<D, G, U>(t, tid, g, min(G * U, e1 - b), leader, tb, acc);
       }
-    } else {
-    for (int j0 = 0; j0 < n; j0 += G * U) {  // :151-167, j ascending
-      double t[U][D];
+    } else if (!DOMAIN_ONLY) {
+      for (int j0 = 0; j0 < n; j0 += G * U) {  // :151-167, j ascending
+        double t[U][D];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = j0 + g + G * u;
+        for (int u = 0; u < U; ++u) {
+          const int j = j0 + g + G * u;
 #pragma unroll
-        for (int k = 0; k < D; ++k) t[u][k] = 0.0;
-        if (active && j < n) {
-          const double* xj = &sx[j * W];
-          if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
-            rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
-          else
-            rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+          for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+          if (active && j < n) {
+            const double* xj = &sx[j * W];
+            if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
+              rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+            else
+              rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+          }
         }
+        group_add<D, G, U>(t, tid, g, min(G * U, n - j0), leader, tb, acc);
       }
-      group_add<D, G, U>(t, tid, g, min(G * U, n - j0), leader, tb, acc);
-    }
-    for (int b = e0; b < e1; b += G * U) {  // :169-203, CSR order
-      double t[U][D];
+      for (int b = e0; b < e1; b += G * U) {  // :169-203, CSR order
+        double t[U][D];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = b + g + G * u;
+        for (int u = 0; u < U; ++u) {
+          const int e = b + g + G * u;
 #pragma unroll
-        for (int k = 0; k < D; ++k) t[u][k] = 0.0;
-        if (e < e1) {
-          const double* xj = &sx[ix[e] * W];
-          const double a = c.use_weights ? dx[e] : 1.0;
-          if (row_ok && all_coord_ok<D>(xj))
-            attr_edge<D, true>(xi, xj, a, dip1, c, t[u]);
-          else
-            attr_edge<D, false>(xi, xj, a, dip1, c, t[u]);
+          for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+          if (e < e1) {
+            const double* xj = &sx[ix[e] * W];
+            const double a = c.use_weights ? dx[e] : 1.0;
+            if (row_ok && all_coord_ok<D>(xj))
+              attr_edge<D, true>(xi, xj, a, dip1, c, t[u]);
+            else
+              attr_edge<D, false>(xi, xj, a, dip1, c, t[u]);
+          }
         }
+        group_add<D, G, U>(t, tid, g, min(G * U, e1 - b), leader, tb, acc);
       }
-      group_add<D, G, U>(t, tid, g, min(G * U, e1 - b), leader, tb, acc);
-    }
     }
     if (leader) {  // gravity :205-211 (mag not clamped)
       double m2 = xi[0] * xi[0];
@@ -537,14 +610,14 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
     }
     __syncthreads();
     if (leader) {  // swing + update :214-269
-      double s = 0.0, f2 = 0.0;
+      double s2 = 0.0, f2 = 0.0;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         const double t = fprev[k] - F[k];
-        s = (k == 0) ? t * t : s + t * t;
+        s2 = (k == 0) ? t * t : s2 + t * t;
         f2 = (k == 0) ? F[k] * F[k] : f2 + F[k] * F[k];
       }
-      const double swing = sqrt(s);
+      const double swing = sqrt(s2);
       const double totalF = sqrt(f2);
       double speed = c.ks_gS / (1 + c.gS * sqrt(swing));
       const double cap = c.ksmax / totalF;
@@ -557,44 +630,64 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
     }
   }
   __syncthreads();
-  for (int q = tid; q < n; q += kSmallT)
+  for (int q = tid; q < n; q += T)
 #pragma unroll
     for (int k = 0; k < D; ++k) Xg[(size_t)q * D + k] = sx[q * W + k];
+  if (leader)
+#pragma unroll
+    for (int k = 0; k < D; ++k) Fp[(size_t)i * D + k] = fprev[k];
+  if (DOMAIN_ONLY && tid == 0) *it_state = it;
 }
 
-// lanes per row for n rows in one 1024-thread workgroup
-inline int small_group(int n) {
+// lanes per row for n rows in a T-thread workgroup
+inline int small_group(int n, int T) {
   if (const char* e = std::getenv("GE_SMALL_G")) {  // tuning override
     const int g = std::atoi(e);
-    if ((g == 1 || g == 2 || g == 4 || g == 8 || g == 16) && n * g <= kSmallT) return g;
+    if ((g == 1 || g == 2 || g == 4 || g == 8 || g == 16) && n * g <= T) return g;
   }
   int G = 1;
-  while (G < 16 && n * G * 2 <= kSmallT) G *= 2;
+  while (G < 16 && n * G * 2 <= T) G *= 2;
   return G;
 }
 
+constexpr int kSmallFastT = 1024;  // domain-only kernel
+constexpr int kSmallGenT = 512;    // general kernel
+
+// Fp: n*D scratch, it_state: one int (device).
 template <int D>
 void launch_small(hipStream_t s, int n, int nnz, const int* ip, const int* ix, const double* dx,
-                  const double* dp1, double* X, int iterations, const FaConst& c) {
-  const bool staged = nnz <= kSmallNnz;
-  switch (small_group(n) * 2 + (staged ? 1 : 0)) {
-#define GE_SMALL(GG, ST)                                                                    \
-  case GG * 2 + ST:                                                                         \
-    hipLaunchKernelGGL((fa_small_strict<D, GG, 1, ST == 1>), dim3(1), dim3(kSmallT), 0, s, n, \
-                       ip, ix, dx, dp1, X, iterations, c);                                  \
-    break;
-    GE_SMALL(1, 0)
-    GE_SMALL(2, 0)
-    GE_SMALL(4, 0)
-    GE_SMALL(8, 0)
-    GE_SMALL(16, 0)
-    GE_SMALL(1, 1)
-    GE_SMALL(2, 1)
-    GE_SMALL(4, 1)
-    GE_SMALL(8, 1)
-    GE_SMALL(16, 1)
-#undef GE_SMALL
-  }
+                  const double* dp1, double* X, double* Fp, int* it_state, int iterations,
+                  const FaConst& c) {
+  GE_HIP(hipMemsetAsync(Fp, 0, sizeof(double) * (size_t)n * D, s));
+  GE_HIP(hipMemsetAsync(it_state, 0, sizeof(int), s));
+  const bool staged = nnz <= small_nnz_cap(D);
+  int stop_at = iterations;  // test hook: hand over to the general kernel there
+  if (const char* e = std::getenv("GE_SMALL_HANDOVER")) stop_at = std::atoi(e);
+  auto go = [&](auto GG, auto TT, auto ST, auto DO) {
+    hipLaunchKernelGGL((fa_small_strict<D, decltype(GG)::value, decltype(TT)::value,
+                                        decltype(ST)::value, decltype(DO)::value>),
+                       dim3(1), dim3(decltype(TT)::value), 0, s, n, ip, ix, dx, dp1, X, Fp,
+                       it_state, iterations, stop_at, c);
+  };
+  using F = std::false_type;
+  using Tt = std::true_type;
+  auto by_group = [&](int G, auto TT, auto DO) {
+    auto by_stage = [&](auto GG) {
+      if (staged) go(GG, TT, Tt(), DO);
+      else go(GG, TT, F(), DO);
+    };
+    switch (G) {
+      case 16: by_stage(std::integral_constant<int, 16>()); break;
+      case 8: by_stage(std::integral_constant<int, 8>()); break;
+      case 4: by_stage(std::integral_constant<int, 4>()); break;
+      case 2: by_stage(std::integral_constant<int, 2>()); break;
+      default: by_stage(std::integral_constant<int, 1>()); break;
+    }
+  };
+  // the domain-only kernel has the linear attraction only (linlog == 0, delta == 1)
+  if (!std::getenv("GE_SMALL_GENERAL_ONLY") && !c.linlog && c.delta == 1.0)
+    by_group(small_group(n, kSmallFastT), std::integral_constant<int, kSmallFastT>(), Tt());
+  by_group(small_group(n, kSmallGenT), std::integral_constant<int, kSmallGenT>(), F());
 }
 
 // ---------------------------------------------------------------------------
@@ -753,13 +846,14 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
   if (n <= 0 || iterations <= 0) return;
   hipStream_t s = ctx->stream;
   if (n <= kSmallMax && p.mode == GE_MODE_STRICT) {
-    DevBuf<double> dp1(n);
+    DevBuf<double> dp1(n), fp((size_t)n * dim);
+    DevBuf<int> it_state(1);
     hipLaunchKernelGGL(degp1_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, d_ip, d_dx,
                        p.use_weights, dp1.p);
     FaConst c = make_const(p);
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
-      launch_small<D>(s, n, nnz, d_ip, d_ix, d_dx, dp1.p, d_x, iterations, c);
+      launch_small<D>(s, n, nnz, d_ip, d_ix, d_dx, dp1.p, d_x, fp.p, it_state.p, iterations, c);
     });
     GE_HIP(hipGetLastError());
     GE_HIP(hipStreamSynchronize(s));

@@ -90,8 +90,18 @@ __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __
   }
 }
 
-// Attraction along one CSR entry (:169-203): t = x_j - x_i.
-template <int D, bool SHARED>
+// attraction_mag for linlog == 0 and delta == 1 (the defaults): no log / pow
+// code, which keeps register-tight kernels within their budget.
+__device__ __forceinline__ double attraction_mag_linear(double dis, double a, double dip1,
+                                                        const FaConst& c) {
+  double f = dis * a;
+  if (c.nohubs) f = f / dip1;
+  return c.attract * f;
+}
+
+// Attraction along one CSR entry (:169-203): t = x_j - x_i.  LINEAR: the caller
+// guarantees linlog == 0 and delta == 1.
+template <int D, bool SHARED, bool LINEAR = false>
 __device__ __forceinline__ void attr_edge(const double (&xi)[D], const double* __restrict__ xj,
                                           double a, double dip1, const FaConst& c,
                                           double (&acc)[D]) {
@@ -102,7 +112,7 @@ __device__ __forceinline__ void attr_edge(const double (&xi)[D], const double* _
 #pragma unroll
   for (int k = 1; k < D; ++k) s = s + t[k] * t[k];
   const double dis = clamp_eps(SHARED ? (s == 0.0 ? 0.0 : sqrt_normal(s)) : sqrt(s));
-  const double Fa = attraction_mag(dis, a, dip1, c);
+  const double Fa = LINEAR ? attraction_mag_linear(dis, a, dip1, c) : attraction_mag(dis, a, dip1, c);
   if (SHARED) {
     const Recip rc = recip_of(dis);
 #pragma unroll

@@ -17,7 +17,7 @@ for n, m in [(127, 2500), (127, 8000), (300, 6000), (600, 12000)]:
     X0 = G.random_coords(nn, 3, seed=2)
     ref = None
     for g, u in [(g, u) for g in (1, 2, 4, 8, 16) for u in (1,)]:
-        if nn * g > 512:
+        if nn * g > 1024:
             continue
         os.environ["GE_SMALL_G"] = str(g)
         os.environ["GE_SMALL_U"] = str(u)

@@ -87,6 +87,31 @@ def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
     assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3), want)
 
 
+@pytest.mark.parametrize("hook", [("GE_SMALL_GENERAL_ONLY", "1"), ("GE_SMALL_HANDOVER", "37"),
+                                  ("GE_SMALL_HANDOVER", "0")])
+def test_fa_small_kernel_handover(ctx, oracle, monkeypatch, hook):
+    """The coarsest-level path is a domain-only kernel followed by the general
+    kernel from the iteration it stopped at; force the general kernel from the
+    start and a hand-over in the middle (coordinates and previous forces cross)."""
+    monkeypatch.setenv(*hook)
+    A = G.largest_component(G.rmat(300, 1500, seed=12))
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=3)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=80)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=80), want)
+
+
+def test_fa_small_kernel_out_of_domain_start(ctx, oracle):
+    """A coordinate below 2^-200 starts outside the shared-reciprocal domain: the
+    domain-only kernel stops at once and the general kernel runs every step."""
+    A = G.largest_component(G.rmat(200, 900, seed=5))
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 2, seed=4)
+    X0[3, 1] = 1e-70
+    want = oracle.force_atlas(A, 2, coords=X0, iterations=25)
+    assert np.array_equal(ctx.force_atlas(A, 2, coords=X0, iterations=25), want)
+
+
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
     # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
