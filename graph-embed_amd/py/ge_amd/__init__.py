@@ -82,6 +82,8 @@ _SIGS = {
     "ge_csr_shape": (ctypes.c_int, [_vp, _ip, _ip, ctypes.POINTER(ctypes.c_longlong)]),
     "ge_csr_copy": (ctypes.c_int, [_vp, _i32p, _vp, _vp]),
     "ge_csr_free": (ctypes.c_int, [_vp]),
+    "ge_modularity_device": (ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, _vp,
+                                            ctypes.POINTER(ctypes.c_double)]),
     "ge_modularity": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _i32p,
                                      ctypes.POINTER(ctypes.c_double)]),
     "ge_embed": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _i32p, _f64p,
@@ -222,6 +224,20 @@ class Context:
             np.ascontiguousarray(r_A, dtype=np.float64), X.reshape(-1), dim, iterations,
             ctypes.byref(p)))
         return X
+
+    def modularity(self, A, vertex_A, m):
+        """partition::modularity with the O(nnz) pass on the device
+        (ge_modularity_device); same bits as the host ge_amd.modularity."""
+        import torch
+        ip, ix, dx = _csr(A)
+        dev = torch.device("cuda", self.device)
+        t = [torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+             for a in (ip, ix, dx, np.asarray(vertex_A, dtype=np.int32))]
+        q = ctypes.c_double()
+        _check(lib().ge_modularity_device(self.h, len(ip) - 1, _vp(t[0].data_ptr()),
+                                          _vp(t[1].data_ptr()), _vp(t[2].data_ptr()), m,
+                                          _vp(t[3].data_ptr()), ctypes.byref(q)))
+        return q.value
 
     def ptap(self, A, PT):
         ip, ix, dx = _csr(A)

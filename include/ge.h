@@ -165,6 +165,11 @@ int ge_csr_free(ge_csr* c);
 /* ---- modularity (src/partitioner.cpp:69-114) ---- */
 int ge_modularity(int n, const int* indptr, const int* indices, const double* data,
                   int m, const int* vertex_A, double* q);
+/* The same with the CSR and vertex_A on the device (O(nnz) pass as 64-bit integer
+ * sums -- exact, the weights being truncated to int -- then the O(M) final sum on
+ * the host in the reference's order).  Same result bits as ge_modularity. */
+int ge_modularity_device(ge_ctx* ctx, int n, const int* d_indptr, const int* d_indices,
+                         const double* d_data, int m, const int* d_vertex_A, double* q);
 
 /* ---- multilevel embed ----
  * Replaces partition::embed(As, P_Ts, d) (include/embed.hpp:70-72,

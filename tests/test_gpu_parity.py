@@ -355,3 +355,18 @@ def test_faml_plan_aggregate_subsets_compose(ctx, oracle, world):
         ctx.sync()
         plan.close()
     assert np.array_equal(X.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("weights", ["unit", "fractional"])
+def test_modularity_device_matches_host(ctx, oracle, weights):
+    """ge_modularity_device (integer atomics + host final sum) gives the host
+    ge_modularity's bits, truncation of weights to int included."""
+    A = G.largest_component(G.rmat(4000, 30000, seed=21))
+    if weights == "fractional":
+        A = (A[0], A[1], np.random.RandomState(3).uniform(0.2, 3.9, len(A[1])))
+    for PT in oracle.partition(A, 0.125)[:3]:
+        vA = ge.vertex_of(PT)
+        m = PT[2]
+        want = ge.modularity(A, vA, m)
+        assert ctx.modularity(A, vA, m) == want
+        A = ctx.ptap(A, PT)
