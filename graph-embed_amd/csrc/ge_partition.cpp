@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <iostream>
 #include <limits>
+#include <new>
 #include <numeric>
 #include <vector>
 
@@ -40,129 +41,200 @@
 namespace ge {
 namespace {
 
-// int -> double map: entries kept dense (keys_/vals_, iteration touches live
-// entries only), located through an open-addressing index table (linear
-// probing, tombstones).  Erase moves the last entry into the hole.
+// int -> double map: entries kept dense (iteration touches live entries only).
+// Up to kSmall entries live inline in the object (most vertices of a
+// power-law graph: one cache line, no pointer chase); larger maps keep
+// keys/vals arrays on the heap located through an open-addressing index table
+// (linear probing, tombstones).  Erase moves the last entry into the hole.
 class NbrMap {
  public:
+  static constexpr int kSmall = 3;
   static constexpr int kEmpty = -1, kTomb = -2;
-  int size() const { return (int)keys_.size(); }
+  NbrMap() = default;
+  NbrMap(const NbrMap&) = delete;
+  NbrMap& operator=(const NbrMap&) = delete;
+  ~NbrMap() { clear(); }
+  int size() const { return size_; }
+  const int* keys() const { return big() ? u_.b.keys : u_.s.k; }
+  const double* vals() const { return big() ? u_.b.vals : u_.s.v; }
 
   void reserve(int want) {
-    keys_.reserve(want);
-    vals_.reserve(want);
-    int cap = 4;
-    while (cap < 2 * want) cap <<= 1;
-    if (cap > (int)table_.size()) rehash(cap);
+    if (want > kSmall) make_big(want);
   }
   // first insertion wins (std::map::insert semantics)
   void insert_new(int k, double v) {
-    grow_if_needed();
-    const int at = probe(k);
-    if (table_[at] >= 0) return;
-    place(at, k, v);
+    if (index_of(k) >= 0) return;
+    append(k, v);
   }
   // m[k] += v (operator[] then +=: 0.0 + v for a new key)
   void add(int k, double v) {
-    grow_if_needed();
-    const int at = probe(k);
-    if (table_[at] >= 0) {
-      vals_[table_[at]] += v;
+    const int x = index_of(k);
+    if (x >= 0) {
+      mvals()[x] += v;
       return;
     }
-    place(at, k, 0.0 + v);
+    append(k, 0.0 + v);
   }
   const double* find(int k) const {
-    const int at = locate(k);
-    return at < 0 ? nullptr : &vals_[table_[at]];
+    const int x = index_of(k);
+    return x < 0 ? nullptr : vals() + x;
   }
   void erase(int k) {
+    if (!big()) {
+      for (int x = 0; x < size_; ++x)
+        if (u_.s.k[x] == k) {
+          --size_;
+          u_.s.k[x] = u_.s.k[size_];
+          u_.s.v[x] = u_.s.v[size_];
+          return;
+        }
+      return;
+    }
     const int at = locate(k);
     if (at < 0) return;
-    const int idx = table_[at];
-    table_[at] = kTomb;
-    const int last = (int)keys_.size() - 1;
+    int* t = u_.b.table;
+    const int idx = t[at];
+    t[at] = kTomb;
+    const int last = size_ - 1;
     if (idx != last) {
-      table_[locate(keys_[last])] = idx;
-      keys_[idx] = keys_[last];
-      vals_[idx] = vals_[last];
+      t[locate(u_.b.keys[last])] = idx;
+      u_.b.keys[idx] = u_.b.keys[last];
+      u_.b.vals[idx] = u_.b.vals[last];
     }
-    keys_.pop_back();
-    vals_.pop_back();
+    --size_;
   }
   // visit entries [b, e) of the dense order (for splitting one map across threads)
   template <class F>
   void for_range(int b, int e, F&& f) const {
-    for (int x = b; x < e; ++x) f(keys_[x], vals_[x]);
+    const int* kk = keys();
+    const double* vv = vals();
+    for (int x = b; x < e; ++x) f(kk[x], vv[x]);
   }
   template <class F>
   void for_each(F&& f) const {
-    for (size_t x = 0; x < keys_.size(); ++x) f(keys_[x], vals_[x]);
+    for_range(0, size_, f);
   }
   void clear() {
-    std::vector<int>().swap(keys_);
-    std::vector<double>().swap(vals_);
-    std::vector<int>().swap(table_);
-    used_ = 0;
+    if (big()) {
+      std::free(u_.b.keys);
+      std::free(u_.b.vals);
+      std::free(u_.b.table);
+    }
+    size_ = kcap_ = tcap_ = used_ = 0;
   }
 
  private:
+  struct Small {
+    int k[kSmall];
+    double v[kSmall];
+  };
+  struct Big {
+    int* keys;
+    double* vals;
+    int* table;
+  };
+  bool big() const { return kcap_ > 0; }
+  double* mvals() { return big() ? u_.b.vals : u_.s.v; }
   static int hash(int k) { return (int)(((uint32_t)k * 2654435761u) >> 1); }
+  int index_of(int k) const {
+    if (!big()) {
+      for (int x = 0; x < size_; ++x)
+        if (u_.s.k[x] == k) return x;
+      return -1;
+    }
+    const int at = locate(k);
+    return at < 0 ? -1 : u_.b.table[at];
+  }
   // table slot holding k, or -1
   int locate(int k) const {
-    if (table_.empty()) return -1;
-    const int mask = (int)table_.size() - 1;
+    const int mask = tcap_ - 1;
+    const int* t = u_.b.table;
     for (int h = hash(k) & mask;; h = (h + 1) & mask) {
-      const int t = table_[h];
-      if (t == kEmpty) return -1;
-      if (t >= 0 && keys_[t] == k) return h;
+      const int x = t[h];
+      if (x == kEmpty) return -1;
+      if (x >= 0 && u_.b.keys[x] == k) return h;
     }
   }
-  // slot of k if present, else the first free slot (tombstone or empty) on its chain
-  int probe(int k) const {
-    const int mask = (int)table_.size() - 1;
-    int tomb = -1;
-    for (int h = hash(k) & mask;; h = (h + 1) & mask) {
-      const int t = table_[h];
-      if (t >= 0) {
-        if (keys_[t] == k) return h;
-      } else if (t == kTomb) {
-        if (tomb < 0) tomb = h;
-      } else {
-        return tomb >= 0 ? tomb : h;
+  void append(int k, double v) {
+    if (!big()) {
+      if (size_ < kSmall) {
+        u_.s.k[size_] = k;
+        u_.s.v[size_] = v;
+        ++size_;
+        return;
       }
+      make_big(2 * kSmall);
     }
-  }
-  void place(int at, int k, double v) {
-    if (table_[at] == kEmpty) ++used_;
-    table_[at] = (int)keys_.size();
-    keys_.push_back(k);
-    vals_.push_back(v);
-  }
-  void grow_if_needed() {
-    if (table_.empty()) {
-      rehash(4);
-    } else if (2 * (used_ + 1) > (int)table_.size()) {
+    if (size_ == kcap_) {
+      kcap_ *= 2;
+      u_.b.keys = static_cast<int*>(std::realloc(u_.b.keys, sizeof(int) * kcap_));
+      u_.b.vals = static_cast<double*>(std::realloc(u_.b.vals, sizeof(double) * kcap_));
+      if (!u_.b.keys || !u_.b.vals) throw std::bad_alloc();
+    }
+    if (2 * (used_ + 1) > tcap_) {
       int cap = 4;
-      while (cap < 4 * ((int)keys_.size() + 1)) cap <<= 1;  // load <= 1/4 after rehash
+      while (cap < 4 * (size_ + 1)) cap <<= 1;  // load <= 1/4 after rehash
       rehash(cap);
     }
+    // first free slot on k's chain (k is absent)
+    const int mask = tcap_ - 1;
+    int* t = u_.b.table;
+    int at = hash(k) & mask;
+    while (t[at] >= 0) at = (at + 1) & mask;
+    if (t[at] == kEmpty) ++used_;
+    t[at] = size_;
+    u_.b.keys[size_] = k;
+    u_.b.vals[size_] = v;
+    ++size_;
+  }
+  void make_big(int want) {
+    if (big()) {
+      if (want <= kcap_) return;
+      u_.b.keys = static_cast<int*>(std::realloc(u_.b.keys, sizeof(int) * want));
+      u_.b.vals = static_cast<double*>(std::realloc(u_.b.vals, sizeof(double) * want));
+      if (!u_.b.keys || !u_.b.vals) throw std::bad_alloc();
+      kcap_ = want;
+      int cap = 4;
+      while (cap < 2 * want) cap <<= 1;
+      if (cap > tcap_) rehash(cap);
+      return;
+    }
+    Small old = u_.s;
+    const int n = size_;
+    kcap_ = std::max(want, 2 * kSmall);
+    u_.b.keys = static_cast<int*>(std::malloc(sizeof(int) * kcap_));
+    u_.b.vals = static_cast<double*>(std::malloc(sizeof(double) * kcap_));
+    u_.b.table = nullptr;
+    if (!u_.b.keys || !u_.b.vals) throw std::bad_alloc();
+    for (int x = 0; x < n; ++x) {
+      u_.b.keys[x] = old.k[x];
+      u_.b.vals[x] = old.v[x];
+    }
+    int cap = 4;
+    while (cap < 2 * kcap_) cap <<= 1;
+    tcap_ = 0;
+    rehash(cap);
   }
   void rehash(int cap) {
-    std::vector<int> t(cap, kEmpty);
+    int* t = static_cast<int*>(std::malloc(sizeof(int) * cap));
+    if (!t) throw std::bad_alloc();
+    std::fill(t, t + cap, kEmpty);
     const int mask = cap - 1;
-    for (size_t x = 0; x < keys_.size(); ++x) {
-      int at = hash(keys_[x]) & mask;
+    for (int x = 0; x < size_; ++x) {
+      int at = hash(u_.b.keys[x]) & mask;
       while (t[at] != kEmpty) at = (at + 1) & mask;
-      t[at] = (int)x;
+      t[at] = x;
     }
-    table_.swap(t);
-    used_ = (int)keys_.size();
+    std::free(u_.b.table);
+    u_.b.table = t;
+    tcap_ = cap;
+    used_ = size_;
   }
-  std::vector<int> keys_;
-  std::vector<double> vals_;
-  std::vector<int> table_;
-  int used_ = 0;  // table slots not kEmpty
+  union {
+    Small s;
+    Big b;
+  } u_;
+  int size_ = 0, kcap_ = 0, tcap_ = 0, used_ = 0;
 };
 
 struct Bitmap {
@@ -254,6 +326,12 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   // now has none -- exactly what its rescan would find -- and gets v back at
   // the end of the round if v survives; the others rescan.
   std::vector<std::pair<int, int>> lost, pending, demoted;
+  // pass >= 2 scans skip busy neighbours; up to kSkip of them are remembered so
+  // the vertex can take them back at the end of the round without a rescan
+  // (skipn = number skipped; > kSkip: rescan)
+  constexpr int kSkip = 8;
+  std::vector<int> skipv((size_t)n * kSkip, -1), skipn(n, 0);
+  std::vector<char> late_scan(n, 0);
   long long ustat = 0;
   auto consume_busy = [&](int v) {
     for (int k : watch[v]) {
@@ -289,6 +367,10 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     for (const auto& kv : pending) {
       const int k = kv.first, v = kv.second;
       if (dirty[k] || dead[k] || arg[k] != v) continue;
+      if (late_scan[k]) {  // its skip record would not cover v: rescan
+        mark(k);
+        continue;
+      }
       const int sidx = second_idx[k];
       double eta;
       if (prof) {
@@ -371,8 +453,9 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   double t_scan = 0, t_resolve = 0, t_merge = 0, t_pop = 0, t_cls = 0, t_par = 0;
   double t_snap = 0, t_swap = 0, t_lost = 0;
   long long rescans = 0, slots_scanned = 0, slots_big = 0, live_scanned = 0;
+  long long hist_n[21] = {0}, hist_e[21] = {0}, hist_p2 = 0;
   int rounds = 0;
-  std::vector<int> todo, keep_dirty, late, big, small_todo;
+  std::vector<int> todo, keep_dirty, late, late_fix, big, small_todo;
   int M_prev = M;
   do {
     ++rounds;
@@ -415,10 +498,14 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
           }
         }
       };
-      auto scan_range = [&](int i, int b, int e, Top2& t) {
+      auto scan_range = [&](int i, int b, int e, Top2& t, int* sk) {
         const double ai = alpha[i];
         adj[i].for_range(b, e, [&](int j, double w) {
-          if (busy[j]) return;
+          if (busy[j]) {
+            if (sk[kSkip] < kSkip) sk[sk[kSkip]] = j;
+            ++sk[kSkip];
+            return;
+          }
           t.offer(2 * (w / T - ai * alpha[j]), j);
         });
       };
@@ -434,6 +521,11 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
         const int cap = adj[todo[x]].size();
         (cap > 4096 ? big : small_todo).push_back(todo[x]);
         if (prof) {
+          int bkt = 0;
+          while ((2 << bkt) <= cap && bkt < 20) ++bkt;
+          hist_n[bkt] += 1;
+          hist_e[bkt] += cap;
+          if (late_scan[todo[x]] == 0 && pass > 0) ++hist_p2;
           slots_scanned += cap;
           if (cap > 8192) slots_big += cap;
           live_scanned += adj[todo[x]].size();
@@ -443,18 +535,29 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
 #pragma omp parallel for schedule(dynamic, 64)
       for (int x = 0; x < nsm; ++x) {
         Top2 t;
+        int sk[kSkip + 1];
+        sk[kSkip] = 0;
         const int i = small_todo[x];
-        scan_range(i, 0, adj[i].size(), t);
+        scan_range(i, 0, adj[i].size(), t, sk);
         store(i, t);
+        for (int q = 0; q < std::min(sk[kSkip], kSkip); ++q) skipv[(size_t)i * kSkip + q] = sk[q];
+        skipn[i] = sk[kSkip];
       }
       for (int i : big) {  // one large neighbourhood split across threads
         const int cap = adj[i].size();
+        skipn[i] = 0;
         Top2 acc;
 #pragma omp parallel
         {
           Top2 t;
+          int sk[kSkip + 1];
+          sk[kSkip] = 0;
 #pragma omp for schedule(static) nowait
-          for (int b = 0; b < cap; b += 1024) scan_range(i, b, std::min(cap, b + 1024), t);
+          for (int b = 0; b < cap; b += 1024) scan_range(i, b, std::min(cap, b + 1024), t, sk);
+          if (sk[2] > 0) {
+#pragma omp atomic
+            skipn[i] += kSkip + 1;  // a split scan does not keep the ids: rescan
+          }
 #pragma omp critical
           {
             if (t.i1 >= 0) acc.offer(t.e1, t.i1);
@@ -469,7 +572,10 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
         const int i = todo[x];
         set_cand(i);
         if (arg[i] >= 0) watch[arg[i]].push_back(i);
-        if (pass > 0) late.push_back(i);  // scanned while this round's pairs were busy
+        if (pass > 0) {  // scanned while this round's pairs were busy
+          late.push_back(i);
+          late_scan[i] = 1;
+        }
       }
       const auto t1 = now();
       t_scan += secs(t0, t1);
@@ -535,7 +641,11 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
     // vertices scanned in passes >= 2 excluded this round's busy pairs; the
     // surviving ones become available again now
     mcur = 4;
-    for (int v : late) mark(v);
+    for (int v : late) {
+      late_scan[v] = 0;
+      if (skipn[v] > kSkip) mark(v);
+      else if (!dirty[v] && !dead[v]) late_fix.push_back(v);
+    }
     late.clear();
     Q += dQ;
     M_prev = M;
@@ -611,6 +721,37 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
       set_cand(k);
     }
     demoted.clear();
+    // late scans: the skipped (busy) neighbours come back.  The scan's top-2
+    // is exact over the others, whose etas did not change (none of them merged
+    // this round, and a merge touching the vertex's adjacency made it dirty).
+    for (int k : late_fix) {
+      if (dirty[k] || dead[k]) continue;
+      bool redo = false;
+      for (int q = 0; q < skipn[k] && !redo; ++q) {
+        const int u = skipv[(size_t)k * kSkip + q];
+        double eta;
+        if (dead[u] || !eta_of(k, u, eta)) {
+          redo = true;
+          break;
+        }
+        if (arg[k] < 0 || eta > best[k] || (eta == best[k] && u < arg[k])) {
+          second[k] = best[k];
+          second_idx[k] = arg[k];
+          best[k] = eta;
+          arg[k] = u;
+        } else if (second_idx[k] < 0 || eta > second[k] || (eta == second[k] && u < second_idx[k])) {
+          second[k] = eta;
+          second_idx[k] = u;
+        }
+      }
+      if (redo) {
+        mark(k);
+        continue;
+      }
+      set_cand(k);
+      if (arg[k] >= 0) watch[arg[k]].push_back(k);
+    }
+    late_fix.clear();
     t_pop += secs(t3, now());
     if (prof && std::getenv("GE_PROFILE_ROUNDS"))
       std::fprintf(stderr, "round %d alive %d merges %zu rescans_total %lld\n", rounds, M,
@@ -625,6 +766,12 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
   if (prof)
     std::fprintf(stderr, "scan split: classify %.3fs parallel %.3fs; slots %lld (big maps %lld), live entries %lld\n",
                  t_cls, t_par, slots_scanned, slots_big, live_scanned);
+  if (prof) {
+    std::fprintf(stderr, "rescans by size 2^b: ");
+    for (int b = 0; b < 21; ++b)
+      if (hist_n[b]) std::fprintf(stderr, "[%d] %lld/%lld  ", b, hist_n[b], hist_e[b]);
+    std::fprintf(stderr, " pass2 %lld\n", hist_p2);
+  }
   if (prof)
     std::fprintf(stderr, "snap+pop split: snap %.3fs swap-pop %.3fs lost %.3fs demoted %.3fs\n",
                  t_snap, t_swap, t_lost, t_pop - t_snap - t_swap - t_lost);
