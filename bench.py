@@ -48,9 +48,10 @@ def parse():
     ap.add_argument("--mode", choices=["strict", "fast"], default="strict")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["c2", "c3"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
                     help="c2: single-level forceAtlas (configs[1]); c3: multilevel level-0 "
-                         "forceAtlasMultilevel on the R-MAT LCC hierarchy (configs[2])")
+                         "forceAtlasMultilevel on the R-MAT LCC hierarchy (configs[2]); c4: the "
+                         "same on the 10M-vertex R-MAT (configs[3]; host partition takes minutes)")
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--ml-iterations", type=int, default=100)
     ap.add_argument("--sweep-slots", action="store_true",
@@ -247,7 +248,8 @@ def run_c3(args, rank, world, local, dev):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C3 (BASELINE.json configs[2]): level-0 forceAtlasMultilevel "
+        "config": {"workload": ("C4 (BASELINE.json configs[3])" if args.workload == "c4" else
+                                "C3 (BASELINE.json configs[2])") + ": level-0 forceAtlasMultilevel "
                                f"({args.ml_iterations} iterations per step) on the LCC of a "
                                f"Graph500 R-MAT ({args.n} ids, {args.draws} draws), "
                                "partition(A, 0.125) first 4 levels, strict fp64",
@@ -322,7 +324,9 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
-    if args.workload == "c3":
+    if args.workload == "c4":  # configs[3]: 10M ids, 80M draws
+        args.n, args.draws = 10_000_000, 80_000_000
+    if args.workload in ("c3", "c4"):
         run_c3(args, rank, world, local, dev)
         if world > 1:
             dist.destroy_process_group()
