@@ -53,6 +53,8 @@ def parse():
                          "forceAtlasMultilevel on the R-MAT LCC hierarchy (configs[2]); c4: the "
                          "same on the 10M-vertex R-MAT (configs[3]; host partition takes minutes)")
     ap.add_argument("--levels", type=int, default=4)
+    ap.add_argument("--partition-cache", default="",
+                    help="c3/c4: directory caching the host partition hierarchy")
     ap.add_argument("--ml-iterations", type=int, default=100)
     ap.add_argument("--sweep-slots", action="store_true",
                     help="c3: also time the streamed path's row-slot / partner variants")
@@ -154,6 +156,35 @@ def cpu_baseline_ml(L, PT, vA, cA, rA, dim, seconds, rank):
             "seconds_per_iteration": per_iter}
 
 
+def partition_levels(L, args):
+    """partition(L, 0.125)[:levels] (host, bit-exact).  With --partition-cache DIR
+    the hierarchy is stored keyed by the generator parameters and a digest of the
+    LCC arrays, and reloaded when both match (the partitioner is deterministic;
+    the cache only skips its minutes of host time at configs[3])."""
+    import ge_amd as ge
+    import hashlib
+    key = None
+    if args.partition_cache:
+        h = hashlib.sha1()
+        for a in L[:2]:
+            h.update(np.ascontiguousarray(a).view(np.uint8))
+        key = os.path.join(args.partition_cache, f"part_n{args.n}_d{args.draws}_s{args.seed}_"
+                                                 f"l{args.levels}_{h.hexdigest()[:16]}.npz")
+        if os.path.exists(key):
+            with np.load(key, allow_pickle=False) as z:
+                return [(z[f"ip{l}"], z[f"ix{l}"], int(z[f"rc{l}"][0]), int(z[f"rc{l}"][1]))
+                        for l in range(int(z["levels"]))], True
+    hier = ge.partition(L, 0.125)[:args.levels]
+    if key:
+        os.makedirs(args.partition_cache, exist_ok=True)
+        arrs = {"levels": np.array(len(hier))}
+        for l, (ip, ix, r, c) in enumerate(hier):
+            arrs.update({f"ip{l}": ip, f"ix{l}": ix, f"rc{l}": np.array([r, c])})
+        np.savez(key + ".tmp.npz", **arrs)
+        os.replace(key + ".tmp.npz", key)
+    return hier, False
+
+
 def run_c3(args, rank, world, local, dev):
     """configs[2] (C3): R-MAT 1M draw -> LCC -> partition(A, 0.125), first 4 P_T
     (examples/embedder.cpp:189-192 pattern) -> P^T A P per level on the device.
@@ -167,10 +198,10 @@ def run_c3(args, rank, world, local, dev):
     t_gen = time.perf_counter() - t0
     n0, nnz0 = len(L[0]) - 1, len(L[1])
     t0 = time.perf_counter()
-    hier = ge.partition(L, 0.125)[:args.levels]
+    hier, cached = partition_levels(L, args)
     t_part = time.perf_counter() - t0
-    log(rank, f"LCC n={n0} nnz={nnz0} (gen {t_gen:.1f}s), partition {t_part:.1f}s, levels "
-              f"{[h[2] for h in hier]}")
+    log(rank, f"LCC n={n0} nnz={nnz0} (gen {t_gen:.1f}s), partition {t_part:.1f}s"
+              f"{' (cache)' if cached else ''}, levels {[h[2] for h in hier]}")
     ctx = ge.Context(local)
     t0 = time.perf_counter()
     As = [L]
@@ -259,7 +290,8 @@ def run_c3(args, rank, world, local, dev):
         "edges_per_s": nnz0 * its,
         "pair_interactions_per_s": pairs * its,
         "finite": finite,
-        "setup_seconds": {"graph": t_gen, "partition_host": t_part, "ptap_device": t_ptap},
+        "setup_seconds": {"graph": t_gen, "partition_host": t_part,
+                          "partition_from_cache": cached, "ptap_device": t_ptap},
         "roofline": {"kernel": "faml_big_repulse (streamed in-aggregate all-pairs, fp64)",
                      "bound": "mfma", "pipe": "fp64 VALU (dense FP64 peak 78.6 TFLOP/s, spec)",
                      "achieved": rep_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
