@@ -691,6 +691,89 @@ void launch_small(hipStream_t s, int n, int nnz, const int* ip, const int* ix, c
 }
 
 // ---------------------------------------------------------------------------
+// STRICT repulsion for small n (n <= grouped_cap, e.g. the coarsest levels of
+// configs[3]): too few rows to fill the chip one lane per row, so G lanes share
+// a row -- they evaluate G consecutive partners at once and the group adds the
+// terms in j order (pipelined_group_sum).  Every block stages all n records in
+// LDS; the exact-division domain is checked once per block.
+
+constexpr int kGrpT = 256;
+constexpr int grouped_cap(int D) { return (D + 1 <= 4) ? 3072 : 1536; }  // <= 96 KiB of records
+inline size_t grouped_lds_bytes(int n, int D) {
+  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kGrpT * D);
+}
+
+template <int D, int G, bool REPEL_ONE>
+__global__ void __launch_bounds__(kGrpT)
+fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
+                   const double* __restrict__ dp1, double repel, double* __restrict__ Frep) {
+  constexpr int W = Rec<D>::W;
+  // dynamic LDS: n records, then the two term buffers (grouped_lds_bytes)
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* rec = smem;
+  double* tb = smem + (size_t)n * W;
+  const int tid = threadIdx.x;
+  const int g = tid % G;
+  const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
+  const bool active = i < re;
+  bool ok = REPEL_ONE || weight_ok(repel);
+  for (int q = tid; q < n; q += kGrpT) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const double v = X[(size_t)q * D + k];
+      rec[q * W + k] = v;
+      ok = ok && coord_ok(v);
+    }
+    const double w = dp1[q];
+    rec[q * W + D] = w;
+    ok = ok && weight_ok(w);
+  }
+  __syncthreads();
+  double xi[D], acc[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xi[k] = active ? rec[i * W + k] : 0.0;
+    acc[k] = 0.0;
+  }
+  const double di = active ? rec[i * W + D] : 1.0;
+  if (__syncthreads_and(ok)) {  // block-uniform: every record in the domain
+    if (G > 1) {
+      pipelined_group_sum<D, G, kGrpT>(n, tid, g, tb, [&](int q, double (&t)[D]) {
+        const int jj = min(q, n - 1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+        rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], repel, t);
+        if (q >= n)
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[k] = 0.0;
+      }, acc);
+    } else {
+      for (int j = 0; j < n; ++j)
+        rep_pair<D, true, REPEL_ONE>(xi, &rec[j * W], di, rec[j * W + D], repel, acc);
+    }
+  } else {
+    const bool row_ok = vertex_ok<D>(xi, di) && (REPEL_ONE || weight_ok(repel));
+    for (int j0 = 0; j0 < n; j0 += G) {
+      double t[1][D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[0][k] = 0.0;
+      const int j = j0 + g;
+      if (j < n) {
+        const double* xj = &rec[j * W];
+        if (row_ok && vertex_ok<D>(xj, rec[j * W + D]))
+          rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], repel, t[0]);
+        else
+          rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], repel, t[0]);
+      }
+      group_add<D, G, 1>(t, tid, g, min(G, n - j0), active && g == 0, tb, acc);
+    }
+  }
+  if (active && g == 0)
+#pragma unroll
+    for (int k = 0; k < D; ++k) Frep[(size_t)(i - rb) * D + k] = acc[k];
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch helpers
 
 constexpr int kRowsPerThreadFast = 4;
@@ -716,6 +799,44 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
     const int tot = rows * D;
     hipLaunchKernelGGL((fa_reduce_parts<D>), dim3((tot + 255) / 256), dim3(256), 0, s, rows, jb,
                        Fpart, Frep);
+    return;
+  }
+  if (n <= grouped_cap(D)) {
+    // lanes per row: aim for >= 64 K threads, at most one wave per row
+    int G = 1;
+    while (G < 64 && (long long)rows * G < 65536) G *= 2;
+    if (const char* e = std::getenv("GE_GRP_G")) {  // tuning / test override
+      const int g = std::atoi(e);
+      if (g >= 1 && g <= 64 && (g & (g - 1)) == 0) G = g;
+    }
+    auto go = [&](auto GG) {
+      constexpr int GC = decltype(GG)::value;
+      const int nb = (rows + kGrpT / GC - 1) / (kGrpT / GC);
+      const size_t lds = grouped_lds_bytes(n, D);
+      if (lds > 65536) {  // above the default dynamic-LDS limit
+        GE_HIP(hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&fa_repulse_grouped<D, GC, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        GE_HIP(hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&fa_repulse_grouped<D, GC, false>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      }
+      if (repel == 1.0)
+        hipLaunchKernelGGL((fa_repulse_grouped<D, GC, true>), dim3(nb), dim3(kGrpT), lds, s, n,
+                           rb, re, X, dp1, repel, Frep);
+      else
+        hipLaunchKernelGGL((fa_repulse_grouped<D, GC, false>), dim3(nb), dim3(kGrpT), lds, s, n,
+                           rb, re, X, dp1, repel, Frep);
+    };
+    switch (G) {
+      case 64: go(std::integral_constant<int, 64>()); break;
+      case 32: go(std::integral_constant<int, 32>()); break;
+      case 16: go(std::integral_constant<int, 16>()); break;
+      case 8: go(std::integral_constant<int, 8>()); break;
+      case 4: go(std::integral_constant<int, 4>()); break;
+      case 2: go(std::integral_constant<int, 2>()); break;
+      default: go(std::integral_constant<int, 1>()); break;
+    }
     return;
   }
   // one block per CU, rows split evenly (rounded to whole 64-row wave slots)
@@ -875,7 +996,32 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
   DevBuf<double> other((size_t)n * dim);
   double* cur = d_x;
   double* nxt = other.p;
-  for (int it = 0; it < iterations; ++it) {
+  int it = 0;
+  // Long runs (the coarsest level's 1e5 iterations) replay a captured graph of
+  // kGraphSteps iterations: host launch overhead would otherwise dominate the
+  // microsecond-scale kernels of a small level.
+  constexpr int kGraphSteps = 32;  // even: the buffers are back in place after a replay
+  if (iterations >= 4 * kGraphSteps && !std::getenv("GE_NO_GRAPH")) {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    GE_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < kGraphSteps; ++k) {
+      plan_step(&pl, cur, nxt);
+      std::swap(cur, nxt);
+    }
+    GE_HIP(hipStreamEndCapture(s, &graph));
+    try {
+      GE_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      for (; it + kGraphSteps <= iterations; it += kGraphSteps) GE_HIP(hipGraphLaunch(exec, s));
+    } catch (...) {
+      if (exec) (void)hipGraphExecDestroy(exec);
+      (void)hipGraphDestroy(graph);
+      throw;
+    }
+    GE_HIP(hipGraphExecDestroy(exec));
+    GE_HIP(hipGraphDestroy(graph));
+  }
+  for (; it < iterations; ++it) {
     plan_step(&pl, cur, nxt);
     std::swap(cur, nxt);
   }

@@ -41,7 +41,9 @@ struct RowClasses {
 // GE_ROWS_MED / GE_ROWS_HEAVY override the class bounds (tuning only).
 inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
                           std::vector<int>& out, int& nheavy, int& nmed, int& nlight) {
-  int med = kMedDeg, heavy = kHeavyDeg;
+  // few rows (a small level): latency, not throughput -- rows of more than 4
+  // entries take a wave (n = 536: attraction 26 -> 13 us per iteration)
+  int med = ids.size() <= 65536 ? 4 : kMedDeg, heavy = kHeavyDeg;
   if (const char* e = std::getenv("GE_ROWS_MED")) med = std::atoi(e);
   if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::atoi(e);
   out.clear();

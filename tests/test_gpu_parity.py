@@ -112,6 +112,17 @@ def test_fa_small_kernel_out_of_domain_start(ctx, oracle):
     assert np.array_equal(ctx.force_atlas(A, 2, coords=X0, iterations=25), want)
 
 
+@pytest.mark.parametrize("grp", ["1", "4", "16", "64"])
+@pytest.mark.parametrize("n,dim", [(700, 3), (1400, 4), (2900, 2)])
+def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim):
+    """Small-n repulsion (fa_repulse_grouped): G lanes per row, in-order group sums."""
+    monkeypatch.setenv("GE_GRP_G", grp)
+    A = G.rmat(n, 6 * n, seed=n)
+    X0 = G.random_coords(n, dim, seed=int(grp))
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=4)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=4), want)
+
+
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
     # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
