@@ -367,6 +367,7 @@ struct FaRows {
 // lane per row (n = 127 gives 16 waves instead of 2).
 
 constexpr int kSmallMax = 512;  // one row group per thread group below
+constexpr int kSmallDefault = 64;
 constexpr int kSmallT = 512;
 constexpr int kSmallNnz = 6144;
 // CSR entries staged in LDS (the 4-D double-buffered term tile leaves less room)
@@ -966,7 +967,12 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
                    const ge_fa_params& p) {
   if (n <= 0 || iterations <= 0) return;
   hipStream_t s = ctx->stream;
-  if (n <= kSmallMax && p.mode == GE_MODE_STRICT) {
+  // One workgroup wins only for tiny levels (n = 14: 3.7 against 12 us per
+  // iteration); from n ~ 100 the multi-block grouped path does (n = 125: 17 us
+  // against 26).  GE_SMALL_MAX moves the bound (tests use it up to kSmallMax).
+  int small_max = kSmallDefault;
+  if (const char* e = std::getenv("GE_SMALL_MAX")) small_max = std::min(kSmallMax, std::atoi(e));
+  if (n <= small_max && p.mode == GE_MODE_STRICT) {
     DevBuf<double> dp1(n), fp((size_t)n * dim);
     DevBuf<int> it_state(1);
     hipLaunchKernelGGL(degp1_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, d_ip, d_dx,

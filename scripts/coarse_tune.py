@@ -11,7 +11,7 @@ import ge_amd as ge  # noqa: E402
 import graphs as G  # noqa: E402
 
 ctx = ge.Context(0)
-cases = [(127, 4000), (500, 10000), (600, 12000), (1068, 30000), (2000, 60000), (5000, 150000)]
+cases = [(16, 60), (40, 200), (127, 4000), (500, 10000), (600, 12000), (1068, 30000), (2000, 60000), (5000, 150000)]
 if os.environ.get("COARSE_ONLY"):
     cases = [c for c in cases if str(c[0]) in os.environ["COARSE_ONLY"].split(",")]
 for n, m in cases:
@@ -23,4 +23,5 @@ for n, m in cases:
     t = time.perf_counter()
     ctx.force_atlas(A, 3, coords=X0, iterations=it)
     dt = time.perf_counter() - t
-    print(f"n={nn} nnz={len(A[1])}: {1e6 * dt / it:.1f} us/iteration", flush=True)
+    print(f"n={nn} nnz={len(A[1])} small_max={os.environ.get('GE_SMALL_MAX', '-')}: "
+          f"{1e6 * dt / it:.1f} us/iteration", flush=True)

@@ -28,7 +28,9 @@ def test_shared_reciprocal_division_is_ieee(ctx):
 # --------------------------------------------------------------------------
 # single-level forceAtlas
 
-def test_fa_golden_supplied_init(ctx, golden):
+@pytest.mark.parametrize("small_max", ["0", "512"])  # grouped multi-block / one workgroup
+def test_fa_golden_supplied_init(ctx, golden, monkeypatch, small_max):
+    monkeypatch.setenv("GE_SMALL_MAX", small_max)
     g = golden("fa_er300_d3")
     A = (g["A_ip"], g["A_ix"], g["A_dx"])
     for it in (1, 10, 100):
@@ -44,7 +46,8 @@ def test_fa_golden_random_init(ctx, golden):
 
 
 @pytest.mark.parametrize("dim", [1, 2, 3, 4])
-def test_fa_small_kernel_dims(ctx, oracle, dim):
+def test_fa_small_kernel_dims(ctx, oracle, monkeypatch, dim):
+    monkeypatch.setenv("GE_SMALL_MAX", "512")
     A = G.erdos_renyi(97, 0.06, seed=dim)
     X0 = G.random_coords(97, dim, seed=dim)
     want = oracle.force_atlas(A, dim, coords=X0, iterations=30)
@@ -94,6 +97,7 @@ def test_fa_small_kernel_handover(ctx, oracle, monkeypatch, hook):
     kernel from the iteration it stopped at; force the general kernel from the
     start and a hand-over in the middle (coordinates and previous forces cross)."""
     monkeypatch.setenv(*hook)
+    monkeypatch.setenv("GE_SMALL_MAX", "512")
     A = G.largest_component(G.rmat(300, 1500, seed=12))
     n = len(A[0]) - 1
     X0 = G.random_coords(n, 3, seed=3)
@@ -101,9 +105,11 @@ def test_fa_small_kernel_handover(ctx, oracle, monkeypatch, hook):
     assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=80), want)
 
 
-def test_fa_small_kernel_out_of_domain_start(ctx, oracle):
+@pytest.mark.parametrize("small_max", ["0", "512"])
+def test_fa_small_kernel_out_of_domain_start(ctx, oracle, monkeypatch, small_max):
     """A coordinate below 2^-200 starts outside the shared-reciprocal domain: the
     domain-only kernel stops at once and the general kernel runs every step."""
+    monkeypatch.setenv("GE_SMALL_MAX", small_max)
     A = G.largest_component(G.rmat(200, 900, seed=5))
     n = len(A[0]) - 1
     X0 = G.random_coords(n, 2, seed=4)
