@@ -8,7 +8,8 @@
 //   medium (deg <= kHeavyDeg)  one wave per row: 64 terms at a time into LDS,
 //                              then every lane adds them in order (same chain,
 //                              broadcast reads);
-//   heavy                      one block per row, kHeavyU*256 terms per chunk.
+//   heavy                      one block per row: three waves evaluate the next
+//                              chunk while the first adds the current one.
 // A term computed alone is 0 + t, equal to t up to the sign of zero; the
 // accumulator starts at +0 and a round-to-nearest sum is -0 only when both
 // operands are, so it is never -0 and adding the stored term later gives the
@@ -29,7 +30,6 @@ namespace ge {
 constexpr int kRowT = 256;
 constexpr int kMedDeg = 32;
 constexpr int kHeavyDeg = 2048;
-constexpr int kHeavyU = 4;
 
 struct RowClasses {
   const int* rows = nullptr;
@@ -121,19 +121,84 @@ __device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* 
   }
 }
 
+// Heavy rows (one 256-thread block per row): waves 1-3 evaluate the next chunk
+// of kSplitChunk terms while wave 0 adds the current chunk in order, so the
+// serial add chain -- the floor for a hub row -- overlaps the gathers.  buf
+// holds two chunks.  Only wave 0's acc is the row's sum.
+constexpr int kSplitU = 4;
+constexpr int kSplitChunk = 192 * kSplitU;  // 3 computing waves x 64 lanes x U
+
+template <int D, class Term>
+__device__ __forceinline__ void ordered_edge_sum_split(int e0, int e1, int tid, double* buf,
+                                                       Term&& term, double (&acc)[D]) {
+  const bool summer = tid < 64;
+  const int w = tid - 64;  // computing lane 0..191
+  // branch-free over the U terms of a lane (indices clamped into the row, the
+  // surplus terms dropped by the summer's count), so the compiler can issue
+  // all U gathers before the arithmetic
+  auto compute = [&](int b, double* dst) {
+    double t[kSplitU][D];
+#pragma unroll
+    for (int u = 0; u < kSplitU; ++u) {
+      const int e = min(b + w + 192 * u, e1 - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+      term(e, t[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kSplitU; ++u)
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[(w + 192 * u) * D + k] = t[u][k];
+  };
+  if (!summer && e0 < e1) compute(e0, buf);
+  __syncthreads();
+  int c = 0;
+  for (int b = e0; b < e1; b += kSplitChunk, ++c) {
+    double* cur = buf + (c & 1) * kSplitChunk * D;
+    if (summer) {
+      // blocks of 8 terms: all 4D 16-byte loads of a block are issued before its
+      // adds, and unrolling lets the next block's loads overlap this block's
+      // add chain (the LDS latency would otherwise sit on the critical path)
+      const int cnt = min(kSplitChunk, e1 - b);
+      int l = 0;
+#pragma unroll 2
+      for (; l + 8 <= cnt; l += 8) {
+        const double2* p = reinterpret_cast<const double2*>(cur + l * D);  // l % 8 == 0
+        double v[8 * D];
+#pragma unroll
+        for (int q = 0; q < 4 * D; ++q) {
+          const double2 x = p[q];
+          v[2 * q] = x.x;
+          v[2 * q + 1] = x.y;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+          for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[t * D + k];
+      }
+      for (; l < cnt; ++l)
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = acc[k] + cur[l * D + k];
+    } else if (b + kSplitChunk < e1) {
+      compute(b + kSplitChunk, buf + ((c + 1) & 1) * kSplitChunk * D);
+    }
+    __syncthreads();
+  }
+}
+
 // P: a row policy with
 //   struct State (holds acc[D] and the edge range e0, e1)
 //   load(row, State&), term(const State&, e, t[D]), finish(State&, bool writer).
 template <int D, class P>
 __global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) {
-  __shared__ __attribute__((aligned(16))) double buf[kRowT * kHeavyU * D];
+  __shared__ __attribute__((aligned(16))) double buf[2 * kSplitChunk * D];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   typename P::State st;
   if (b < L.nheavy) {
     p.load(L.rows[b], st);
-    ordered_edge_sum<D, kRowT, kHeavyU>(
-        st.e0, st.e1, tid, buf, [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
+    ordered_edge_sum_split<D>(st.e0, st.e1, tid, buf,
+                              [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
     p.finish(st, tid == 0);
     return;
   }
