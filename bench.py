@@ -68,9 +68,9 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic_per_launch(kernel_prefix):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes
-    (profiles/*/pmc_fetch*.csv, pmc_write*.csv).  gfx950 correction from
+def pmc_traffic_per_launch(kernel_prefix, workload):
+    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes of
+    the same workload (profiles/*/pmc_fetch_<workload>*.csv, pmc_write_<...>.csv).  gfx950 correction from
     MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a wide coalesced
     read -> bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024."""
     def read(pattern, counter):
@@ -86,8 +86,8 @@ def pmc_traffic_per_launch(kernel_prefix):
             if vals:
                 return sum(vals) / len(vals), path
         return None
-    f = read("pmc_fetch*.csv", "FETCH_SIZE")
-    w = read("pmc_write*.csv", "WRITE_SIZE")
+    f = read(f"pmc_fetch_{workload}*.csv", "FETCH_SIZE")
+    w = read(f"pmc_write_{workload}*.csv", "WRITE_SIZE")
     if not f or not w:
         return None, None
     return (2.0 * f[0] + w[0]) * 1024.0, [os.path.relpath(f[1], REPO), os.path.relpath(w[1], REPO)]
@@ -265,7 +265,7 @@ def run_c3(args, rank, world, local, dev):
     run_ms = e0.elapsed_time(e1) / args.steps
     res_ms, str_ms, _ = plan.kernel_ms()
     rep_ms, rep_launches, rep_pairs = plan.repulse_ms()
-    traffic, traffic_src = pmc_traffic_per_launch("faml_big_repulse")
+    traffic, traffic_src = pmc_traffic_per_launch("faml_big_repulse", args.workload)
     finite = bool(torch.isfinite(X).all().item())
     sizes = np.diff(PT[0]).astype(np.float64)
     pairs = float((sizes * (sizes - 1)).sum())
@@ -428,8 +428,8 @@ def main():
     rep_tflops = FLOPS_PER_PAIR * pairs / (rep_ms * 1e-3) / 1e12 if rep_ms > 0 else 0.0
     attr_bytes = 12 * nnz * rows / n + 52 * rows + 4  # SURVEY 8(d) B_attr, this rank's rows
     att_gbs = attr_bytes / (att_ms * 1e-3) / 1e9 if att_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic_per_launch("fa_repulse")
-    att_traffic, _ = pmc_traffic_per_launch("FaRows")
+    traffic, traffic_src = pmc_traffic_per_launch("fa_repulse", "c2")
+    att_traffic, _ = pmc_traffic_per_launch("FaRows", "c2")
 
     result = {
         "metric": METRIC,
