@@ -285,7 +285,7 @@ __global__ void fa_reduce_parts(int rows, int jblocks, const double* __restrict_
 
 template <int D>
 __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D], double (&acc)[D],
-                                           double dip1, const FaConst& c,
+                                           const double (&fprev)[D], double dip1, const FaConst& c,
                                            double* __restrict__ Fprev,
                                            double* __restrict__ Xnext, bool write = true) {
   double m2 = xi[0] * xi[0];
@@ -302,7 +302,7 @@ __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D],
   double s = 0.0, f2 = 0.0;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    const double t = Fprev[(size_t)li * D + k] - F[k];
+    const double t = fprev[k] - F[k];
     s = (k == 0) ? t * t : s + t * t;
     f2 = (k == 0) ? F[k] * F[k] : f2 + F[k] * F[k];
   }
@@ -330,7 +330,7 @@ struct FaRows {
   FaConst c;
   struct State {
     int i, e0, e1;
-    double xi[D], acc[D], dip1;
+    double xi[D], acc[D], fprev[D], dip1;
     bool row_ok;
   };
   __device__ __forceinline__ void load(int i, State& s) const {
@@ -341,6 +341,7 @@ struct FaRows {
     for (int k = 0; k < D; ++k) {
       s.xi[k] = X[(size_t)i * D + k];
       s.acc[k] = Frep[(size_t)(i - rb) * D + k];
+      s.fprev[k] = Fprev[(size_t)(i - rb) * D + k];  // loaded early: off the row's critical path
     }
     s.dip1 = dp1[i];
     s.row_ok = all_coord_ok<D>(s.xi);
@@ -354,7 +355,7 @@ struct FaRows {
       attr_edge<D, false>(s.xi, xj, a, s.dip1, c, t);
   }
   __device__ __forceinline__ void finish(State& s, bool writer) const {
-    finish_row<D>(s.i, s.i - rb, s.xi, s.acc, s.dip1, c, Fprev, Xnext, writer);
+    finish_row<D>(s.i, s.i - rb, s.xi, s.acc, s.fprev, s.dip1, c, Fprev, Xnext, writer);
   }
 };
 
@@ -871,14 +872,13 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
 }
 
 template <int D>
-void launch_attract(hipStream_t s, const RowClasses& rc, int rb, const int* ip, const int* ix,
-                    const double* dx, const double* X, const double* dp1, const double* Frep,
-                    double* Fprev, double* Xnext, const FaConst& c) {
-  if (rc.grid() == 0) return;
+void launch_attract(hipStream_t s, const RowClasses& rc, RowStreams& rs, int rb, const int* ip,
+                    const int* ix, const double* dx, const double* X, const double* dp1,
+                    const double* Frep, double* Fprev, double* Xnext, const FaConst& c) {
   const FaRows<D> fr{rb, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c};
-  hipLaunchKernelGGL((classed_rows_kernel<D, FaRows<D>>), dim3(rc.grid()), dim3(kRowT), 0, s, rc,
-                     fr);
+  launch_rows<D>(rc, fr, s, rs);
 }
+
 
 }  // namespace
 }  // namespace ge
@@ -897,6 +897,7 @@ struct ge_fa_plan {
   ge::DevBuf<double> dp1, frep, fprev, fpart;
   ge::DevBuf<int> rows;  // rb..re in degree classes (ge_rows.hpp)
   ge::RowClasses rc;
+  ge::RowStreams rstreams;
   int cus = 256;
   bool profiling = false;
   std::vector<hipEvent_t> events;  // 3 per timed step
@@ -923,10 +924,10 @@ static void plan_init(ge_fa_plan* pl) {
       ids[q] = pl->rb + q;
       deg[q] = h_ip[q + 1] - h_ip[q];
     }
-    classify_rows(ids, deg, order, pl->rc.nheavy, pl->rc.nmed, pl->rc.nlight);
-    pl->rows.alloc(rows);
-    pl->rows.upload(order.data(), rows, s);
-    pl->rc.rows = pl->rows.p;
+    classify_rows(ids, deg, order, pl->rc);
+    pl->rows.alloc(order.size());
+    pl->rows.upload(order.data(), order.size(), s);
+    pl->rc.bind(pl->rows.p);
     GE_HIP(hipStreamSynchronize(s));
   }
   hipLaunchKernelGGL(degp1_kernel, dim3((pl->n + 255) / 256), dim3(256), 0, s, pl->n, pl->ip,
@@ -955,7 +956,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
     launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
                         pl->frep.p, pl->fpart.p, pl->cus);
     if (ev) GE_HIP(hipEventRecord(ev[1], s));
-    launch_attract<D>(s, pl->rc, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
+    launch_attract<D>(s, pl->rc, pl->rstreams, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
                       pl->fprev.p, xn, pl->c);
   });
   GE_HIP(hipGetLastError());

@@ -472,7 +472,7 @@ struct FamlRows {
   MlConst c;
   struct State {
     int cpos, a, li, e0, e1;
-    double xi[D], acc[D], dip1, mag;
+    double xi[D], acc[D], fprev[D], dip1, mag;
     Recip rmag;
     bool row_ok, ca_ok;
   };
@@ -487,6 +487,7 @@ struct FamlRows {
     for (int k = 0; k < D; ++k) {
       s.xi[k] = Xc[(size_t)cpos * D + k];
       s.acc[k] = Fscr[(size_t)cpos * D + k];
+      s.fprev[k] = Fprev[(size_t)cpos * D + k];  // loaded early: off the row's critical path
     }
     s.dip1 = DP[cpos];
     s.row_ok = all_coord_ok<D>(s.xi);
@@ -522,7 +523,7 @@ struct FamlRows {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       F[k] = s.acc[k] + unit[k] * c.gravity * s.dip1;
-      Fp[k] = Fprev[(size_t)s.cpos * D + k];
+      Fp[k] = s.fprev[k];
       x[k] = s.xi[k];
     }
     member_update<D>(x, F, Fp, c);
@@ -668,6 +669,7 @@ struct ge_faml_plan {
   size_t off_m = 0, off_l = 0;
   ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge, ecode;
   ge::RowClasses ecls;
+  ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
   double streamed_pairs = 0.0;
@@ -757,11 +759,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       const int v = h_ptix[rows[q]];
       deg[q] = h_ip[v + 1] - h_ip[v];
     }
-    classify_rows(rows, deg, erows, pl->ecls.nheavy, pl->ecls.nmed, pl->ecls.nlight);
+    classify_rows(rows, deg, erows, pl->ecls);
     pl->ecode.alloc(std::max(h_ip[pl->n], 1));
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
-    pl->ecls.rows = pl->erows.p;
+    pl->ecls.bind(pl->erows.p);
   }
   struct Item { int a, r0; double work; };
   std::vector<Item> its;
@@ -884,8 +886,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
         if (re) GE_HIP(hipEventRecord(re[1], ss));
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
                              cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
-        hipLaunchKernelGGL((classed_rows_kernel<D, FamlRows<D>>), dim3(pl->ecls.grid()),
-                           dim3(kRowT), 0, ss, pl->ecls, fr);
+        launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
         std::swap(cur, nxt);
       }
       hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,

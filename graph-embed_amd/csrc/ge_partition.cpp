@@ -554,7 +554,7 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
           sk[kSkip] = 0;
 #pragma omp for schedule(static) nowait
           for (int b = 0; b < cap; b += 1024) scan_range(i, b, std::min(cap, b + 1024), t, sk);
-          if (sk[2] > 0) {
+          if (sk[kSkip] > 0) {
 #pragma omp atomic
             skipn[i] += kSkip + 1;  // a split scan does not keep the ids: rescan
           }

@@ -1,27 +1,36 @@
-// ge_rows.hpp -- degree-classed CSR row kernels with an in-order edge sum.
+// ge_rows.hpp -- CSR row kernels with an in-order edge sum.
 //
 // The reference adds a row's edge terms to its force one after the other in
 // stored order (include/forceatlas.hpp:169-203, :415-467), so a row's sum is a
-// serial chain; but each TERM depends only on the two endpoints.  Rows are
-// therefore split by degree:
-//   light  (deg <= kMedDeg)    one thread per row, terms added as computed;
-//   medium (deg <= kHeavyDeg)  one wave per row: 64 terms at a time into LDS,
-//                              then every lane adds them in order (same chain,
-//                              broadcast reads);
-//   heavy                      one block per row: three waves evaluate the next
-//                              chunk while the first adds the current one.
+// serial chain; but each TERM depends only on the two endpoints.  So the terms
+// are evaluated in parallel and only the adds are serial:
+//   heavy (deg > kTileCap)     one block per row: three waves evaluate the next
+//                              chunk while the first adds the current one;
+//   tiles (many rows)          consecutive rows packed into tiles of <= kTileRows
+//                              rows and <= kTileCap entries: one thread per
+//                              entry evaluates its term into LDS (coalesced
+//                              index reads, every gather of the tile in flight
+//                              at once), then one lane per (row, dimension)
+//                              adds the row's terms in order;
+//   medium / light (few rows, a small level: latency, not throughput)
+//                              one wave per row / one thread per row.
+// In the serial adds, lane k carries dimension k: one dependent add per term.
 // A term computed alone is 0 + t, equal to t up to the sign of zero; the
 // accumulator starts at +0 and a round-to-nearest sum is -0 only when both
 // operands are, so it is never -0 and adding the stored term later gives the
 // reference's bits.
 //
-// One launch covers all three classes: blocks [0, nheavy) take heavy rows
-// (scheduled first: longest chains), then 4 medium rows per block, then 256
-// light rows per block.  `rows` lists heavy, then medium, then light rows.
+// classed_rows_kernel: blocks [0, nheavy) take heavy rows (scheduled first:
+// longest chains), then 4 medium rows per block, then 256 light rows per block.
+// tile_rows_kernel takes the tiles, on the caller's stream, while the heavy
+// rows run beside it on a side stream (launch_rows).  `rows` lists heavy rows, then the tiled rows (in
+// the caller's order, so a tile's CSR rows are usually contiguous), then
+// medium, then light rows; the tile boundaries follow them in the same array.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -30,32 +39,74 @@ namespace ge {
 constexpr int kRowT = 256;
 constexpr int kMedDeg = 32;
 constexpr int kHeavyDeg = 2048;
+#ifndef GE_TILE_ROWS
+#define GE_TILE_ROWS 64
+#endif
+#ifndef GE_TILE_CAP
+#define GE_TILE_CAP 512
+#endif
+#ifndef GE_ROWS_MINBLOCKS
+#define GE_ROWS_MINBLOCKS 1
+#endif
+constexpr int kTileRows = GE_TILE_ROWS;  // <= 128 (two-wave scan)
+constexpr int kTileCap = GE_TILE_CAP;    // entries per tile (multiple of kRowT); longer rows are heavy
+constexpr int kTileMinRows = 65536;  // fewer rows: medium / light classes
 
 struct RowClasses {
   const int* rows = nullptr;
-  int nheavy = 0, nmed = 0, nlight = 0;
+  const int* tile_ptr = nullptr;  // ntiles + 1 offsets into rows
+  int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0;
+  int tile_off = 0;  // where tile_ptr starts in the host array
   int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
+  void bind(const int* dev) {
+    rows = dev;
+    tile_ptr = dev + tile_off;
+  }
 };
 
-// Host: order `ids` (row ids with their degrees) into heavy, medium, light.
-// GE_ROWS_MED / GE_ROWS_HEAVY override the class bounds (tuning only).
+// Host: order `ids` (row ids with their degrees) into classes; `out` gets the
+// row list followed by the tile boundaries (upload all of it, then bind()).
+// GE_ROWS_MED / GE_ROWS_HEAVY / GE_ROWS_TILES override the choices (tuning).
 inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
-                          std::vector<int>& out, int& nheavy, int& nmed, int& nlight) {
+                          std::vector<int>& out, RowClasses& rc) {
+  bool tiles = ids.size() >= (size_t)kTileMinRows;
+  if (const char* e = std::getenv("GE_ROWS_TILES")) tiles = std::atoi(e) != 0;
   // few rows (a small level): latency, not throughput -- rows of more than 4
   // entries take a wave (n = 536: attraction 26 -> 13 us per iteration)
-  int med = ids.size() <= 65536 ? 4 : kMedDeg, heavy = kHeavyDeg;
+  int med = ids.size() <= 65536 ? 4 : kMedDeg, heavy = tiles ? kTileCap : kHeavyDeg;
   if (const char* e = std::getenv("GE_ROWS_MED")) med = std::atoi(e);
-  if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::atoi(e);
+  if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::min(std::atoi(e), tiles ? kTileCap : 1 << 30);
   out.clear();
   for (size_t q = 0; q < ids.size(); ++q)
     if (deg[q] > heavy) out.push_back(ids[q]);
-  nheavy = (int)out.size();
-  for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] > med && deg[q] <= heavy) out.push_back(ids[q]);
-  nmed = (int)out.size() - nheavy;
-  for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] <= med && deg[q] <= heavy) out.push_back(ids[q]);
-  nlight = (int)out.size() - nheavy - nmed;
+  rc.nheavy = (int)out.size();
+  std::vector<int> tp;
+  if (tiles) {
+    int rows = 0, ents = 0;
+    for (size_t q = 0; q < ids.size(); ++q) {
+      if (deg[q] > heavy) continue;
+      if (rows == 0 || rows == kTileRows || ents + deg[q] > kTileCap) {
+        tp.push_back((int)out.size());
+        rows = ents = 0;
+      }
+      out.push_back(ids[q]);
+      ++rows;
+      ents += deg[q];
+    }
+    rc.ntiles = (int)tp.size();
+    tp.push_back((int)out.size());
+    rc.nmed = rc.nlight = 0;
+  } else {
+    rc.ntiles = 0;
+    for (size_t q = 0; q < ids.size(); ++q)
+      if (deg[q] > med && deg[q] <= heavy) out.push_back(ids[q]);
+    rc.nmed = (int)out.size() - rc.nheavy;
+    for (size_t q = 0; q < ids.size(); ++q)
+      if (deg[q] <= med && deg[q] <= heavy) out.push_back(ids[q]);
+    rc.nlight = (int)out.size() - rc.nheavy - rc.nmed;
+  }
+  rc.tile_off = (int)out.size();
+  out.insert(out.end(), tp.begin(), tp.end());
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -64,68 +115,93 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int G>
-__device__ __forceinline__ void group_sync() {
-  if (G == 64)
-    wave_lds_sync();
-  else
-    __syncthreads();
+// Lane k (< D) of the summing wave carries dimension k's running sum; the
+// other lanes shadow lane D-1.  One dependent add per term instead of D, so the
+// serial chain -- the floor for a hub row -- is D times shorter.  Terms sit in
+// LDS dimension-major (buf[k * stride + term]), so a lane's 8 next terms are
+// 4 contiguous 16-byte reads.
+template <int D>
+__device__ __forceinline__ double lane_dim_value(const double (&acc)[D], int kd) {
+  double a = acc[0];
+#pragma unroll
+  for (int k = 1; k < D; ++k)
+    if (kd == k) a = acc[k];
+  return a;
 }
 
-// acc += term(e0) + term(e0+1) + ... in order; G threads (g = 0..G-1) share buf
-// (G*U*D doubles, 16-byte aligned).  The terms are evaluated by all G threads;
-// the ordered adds are done by the group's first wave only (for G = 64: the
-// whole group), whose lanes all end with the same acc -- the other waves'
-// acc is not updated.  Two terms (2D doubles) are read with D 16-byte loads.
-template <int D, int G, int U, class Term>
-__device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int g, double* buf, Term&& term,
+// a += p[0] + p[1] + ... + p[cnt-1], in order (p 16-byte aligned).  Software
+// pipelined: the reads of the next 16 terms are issued before the adds of the
+// current 16, so the LDS latency is hidden behind the dependent add chain
+// (without it every 16 terms paid a full LDS round trip).
+__device__ __forceinline__ double lane_chain(double a, const double* p, int cnt) {
+  constexpr int B = 16, R = B / 2;  // terms per block, 16-byte reads per block
+  const double2* q = reinterpret_cast<const double2*>(p);
+  const int np = cnt / (2 * B);  // pairs of blocks: ping-pong without branches
+  if (np > 0) {
+    double2 x[R], y[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = q[r];
+    for (int b = 0; b < np; ++b) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) y[r] = q[(2 * b + 1) * R + r];
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the adds
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a = a + x[r].x;
+        a = a + x[r].y;
+      }
+      const int b2 = min(2 * b + 2, 2 * np - 1);  // past the end: re-read (unused)
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[r] = q[b2 * R + r];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        a = a + y[r].x;
+        a = a + y[r].y;
+      }
+    }
+  }
+  for (int l = np * 2 * B; l < cnt; ++l) a = a + p[l];
+  return a;
+}
+
+// acc += term(e0) + term(e0+1) + ... in order, by one wave (lane 0..63); buf
+// holds D * 64 * U doubles.  Every lane ends with the full acc.
+template <int D, int U, class Term>
+__device__ __forceinline__ void ordered_edge_sum(int e0, int e1, int lane, double* buf, Term&& term,
                                                  double (&acc)[D]) {
-  const bool summer = G == 64 || g < 64;
-  for (int b = e0; b < e1; b += G * U) {
-    group_sync<G>();  // the previous chunk has been read
+  constexpr int kStride = 64 * U;
+  const int kd = lane < D ? lane : D - 1;
+  double a = lane_dim_value<D>(acc, kd);
+  for (int b = e0; b < e1; b += kStride) {
+    wave_lds_sync();  // the previous chunk has been read
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = b + g + G * u;
+      const int e = b + lane + 64 * u;
       if (e < e1) {
         double t[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
         term(e, t);
 #pragma unroll
-        for (int k = 0; k < D; ++k) buf[(g + G * u) * D + k] = t[k];
+        for (int k = 0; k < D; ++k) buf[k * kStride + lane + 64 * u] = t[k];
       }
     }
-    group_sync<G>();
-    if (summer) {
-      const int cnt = min(G * U, e1 - b);
-      int l = 0;
-#pragma unroll 2
-      for (; l + 1 < cnt; l += 2) {
-        const double2* p = reinterpret_cast<const double2*>(buf + l * D);  // l even: aligned
-        double v[2 * D];
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-          const double2 w = p[q];
-          v[2 * q] = w.x;
-          v[2 * q + 1] = w.y;
-        }
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[k];
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[D + k];
-      }
-      if (l < cnt)
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + buf[l * D + k];
-    }
+    wave_lds_sync();
+    a = lane_chain(a, buf + kd * kStride, min(kStride, e1 - b));
   }
+#pragma unroll
+  for (int k = 0; k < D; ++k) acc[k] = __shfl(a, k);
 }
 
 // Heavy rows (one 256-thread block per row): waves 1-3 evaluate the next chunk
-// of kSplitChunk terms while wave 0 adds the current chunk in order, so the
-// serial add chain -- the floor for a hub row -- overlaps the gathers.  buf
-// holds two chunks.  Only wave 0's acc is the row's sum.
-constexpr int kSplitU = 4;
+// of kSplitChunk terms while wave 0 adds the current one in order, so the
+// serial add chain overlaps the gathers.  buf holds two chunks, each
+// dimension-major.  Only wave 0's acc is the row's sum.
+#ifndef GE_SPLIT_U
+#define GE_SPLIT_U 4
+#endif
+constexpr int kSplitU = GE_SPLIT_U;
 constexpr int kSplitChunk = 192 * kSplitU;  // 3 computing waves x 64 lanes x U
 
 template <int D, class Term>
@@ -148,50 +224,141 @@ __device__ __forceinline__ void ordered_edge_sum_split(int e0, int e1, int tid, 
 #pragma unroll
     for (int u = 0; u < kSplitU; ++u)
 #pragma unroll
-      for (int k = 0; k < D; ++k) dst[(w + 192 * u) * D + k] = t[u][k];
+      for (int k = 0; k < D; ++k) dst[k * kSplitChunk + w + 192 * u] = t[u][k];
   };
+  const int kd = tid < D ? tid : D - 1;
+  double a = lane_dim_value<D>(acc, kd);
   if (!summer && e0 < e1) compute(e0, buf);
   __syncthreads();
   int c = 0;
   for (int b = e0; b < e1; b += kSplitChunk, ++c) {
     double* cur = buf + (c & 1) * kSplitChunk * D;
-    if (summer) {
-      // blocks of 8 terms: all 4D 16-byte loads of a block are issued before its
-      // adds, and unrolling lets the next block's loads overlap this block's
-      // add chain (the LDS latency would otherwise sit on the critical path)
-      const int cnt = min(kSplitChunk, e1 - b);
-      int l = 0;
-#pragma unroll 2
-      for (; l + 8 <= cnt; l += 8) {
-        const double2* p = reinterpret_cast<const double2*>(cur + l * D);  // l % 8 == 0
-        double v[8 * D];
-#pragma unroll
-        for (int q = 0; q < 4 * D; ++q) {
-          const double2 x = p[q];
-          v[2 * q] = x.x;
-          v[2 * q + 1] = x.y;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-#pragma unroll
-          for (int k = 0; k < D; ++k) acc[k] = acc[k] + v[t * D + k];
-      }
-      for (; l < cnt; ++l)
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + cur[l * D + k];
-    } else if (b + kSplitChunk < e1) {
+    if (summer)
+      a = lane_chain(a, cur + kd * kSplitChunk, min(kSplitChunk, e1 - b));
+    else if (b + kSplitChunk < e1)
       compute(b + kSplitChunk, buf + ((c + 1) & 1) * kSplitChunk * D);
-    }
     __syncthreads();
+  }
+  if (summer)
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = __shfl(a, k);
+}
+
+// a += p[0] + ... + p[cnt-1] in order, p 8-byte aligned (8 reads ahead)
+__device__ __forceinline__ double lane_chain_any(double a, const double* p, int cnt) {
+  int l = 0;
+  for (; l + 8 <= cnt; l += 8) {
+    double v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = p[l + t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) a = a + v[t];
+  }
+  for (; l < cnt; ++l) a = a + p[l];
+  return a;
+}
+
+// LDS bytes of the classed kernel (heavy / medium rows) and of a tile.
+template <int D, class P>
+struct RowsLds {
+  static constexpr size_t heavy = sizeof(double) * 2 * kSplitChunk * D;
+  static constexpr size_t medium = sizeof(double) * 4 * 64 * D;
+  static constexpr size_t bytes = heavy > medium ? heavy : medium;
+  static constexpr size_t tile = sizeof(double) * kTileCap * D +
+                                 sizeof(typename P::State) * kTileRows + sizeof(int) * (kTileRows + 2);
+};
+
+// One tile: rows L.rows[r0 .. r1), entries of all of them <= kTileCap.
+template <int D, class P>
+__device__ __forceinline__ void tile_rows(const RowClasses& L, const P& p, int t, char* lds) {
+  using State = typename P::State;
+  double* tb = reinterpret_cast<double*>(lds);  // [D][kTileCap]
+  State* sst = reinterpret_cast<State*>(lds + sizeof(double) * kTileCap * D);
+  int* soff = reinterpret_cast<int*>(lds + sizeof(double) * kTileCap * D + sizeof(State) * kTileRows);
+  const int tid = threadIdx.x;
+  const int r0 = L.tile_ptr[t], nr = L.tile_ptr[t + 1] - r0;
+  // phase 0: row states; exclusive scan of the row lengths (rows < 128: waves 0-1)
+  int len = 0;
+  if (tid < nr) {
+    State st;
+    p.load(L.rows[r0 + tid], st);
+    sst[tid] = st;
+    len = st.e1 - st.e0;
+  }
+  const int lane = tid & 63;
+  int inc = len;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  if (tid == 63) soff[kTileRows + 1] = inc;  // wave 0's total (scratch)
+  __syncthreads();
+  if (tid < 64) soff[tid + 1] = inc;
+  else if (tid < 128) soff[tid + 1] = inc + soff[kTileRows + 1];
+  if (tid == 0) soff[0] = 0;
+  __syncthreads();
+  const int total = soff[nr];
+  // phase 1: one thread per entry; a fixed trip count with the entry index
+  // clamped into the tile, so all of a thread's gathers can be in flight at once
+  if (total > 0) {
+    constexpr int U = kTileCap / kRowT;
+    int es[U], ss[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = min(tid + kRowT * u, total - 1);
+      int lo = 0, hi = nr;  // last s with soff[s] <= q
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (soff[mid] <= q) lo = mid;
+        else hi = mid;
+      }
+      ss[u] = lo;
+      es[u] = q - soff[lo];
+    }
+    double tt[U][D];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const State& st = sst[ss[u]];
+#pragma unroll
+      for (int k = 0; k < D; ++k) tt[u][k] = 0.0;
+      p.term(st, st.e0 + es[u], tt[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (tid + kRowT * u < total)
+#pragma unroll
+        for (int k = 0; k < D; ++k) tb[k * kTileCap + tid + kRowT * u] = tt[u][k];
+  }
+  __syncthreads();
+  // phase 2: one lane per (row, dimension), the row's terms in order
+  for (int x = tid; x < nr * D; x += kRowT) {
+    const int s = x / D, k = x - s * D;
+    const int b = soff[s];
+    sst[s].acc[k] = lane_chain_any(sst[s].acc[k], tb + k * kTileCap + b, soff[s + 1] - b);
+  }
+  __syncthreads();
+  if (tid < nr) {
+    State st = sst[tid];
+    p.finish(st, true);
   }
 }
 
+// Tiles get their own kernel: without the heavy path's registers and LDS it
+// keeps several blocks per CU in flight (the pass is gather-latency bound).
+template <int D, class P>
+__global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p) {
+  __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
+  tile_rows<D>(L, p, blockIdx.x, lds);
+}
+
 // P: a row policy with
-//   struct State (holds acc[D] and the edge range e0, e1)
+//   struct State (holds acc[D] and the edge range e0, e1; trivially copyable)
 //   load(row, State&), term(const State&, e, t[D]), finish(State&, bool writer).
 template <int D, class P>
-__global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) {
-  __shared__ __attribute__((aligned(16))) double buf[2 * kSplitChunk * D];
+__global__ void __launch_bounds__(kRowT, GE_ROWS_MINBLOCKS) classed_rows_kernel(RowClasses L, P p) {
+  __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::bytes];
+  double* buf = reinterpret_cast<double*>(lds);
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   typename P::State st;
@@ -202,21 +369,23 @@ __global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) 
     p.finish(st, tid == 0);
     return;
   }
+  const int r_med = L.tile_off - L.nmed - L.nlight;  // first medium row
   const int mblocks = (L.nmed + 3) / 4;
-  if (b < L.nheavy + mblocks) {
-    const int q = (b - L.nheavy) * 4 + (tid >> 6);
+  const int bm = b - L.nheavy;
+  if (bm < mblocks) {
+    const int q = bm * 4 + (tid >> 6);
     if (q >= L.nmed) return;  // wave-uniform; no block barrier on this path
     const int lane = tid & 63;
-    p.load(L.rows[L.nheavy + q], st);
-    ordered_edge_sum<D, 64, 1>(
+    p.load(L.rows[r_med + q], st);
+    ordered_edge_sum<D, 1>(
         st.e0, st.e1, lane, buf + (tid >> 6) * 64 * D,
         [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
     p.finish(st, lane == 0);
     return;
   }
-  const int q = (b - L.nheavy - mblocks) * kRowT + tid;
+  const int q = (bm - mblocks) * kRowT + tid;
   if (q >= L.nlight) return;
-  p.load(L.rows[L.nheavy + L.nmed + q], st);
+  p.load(L.rows[r_med + L.nmed + q], st);
   for (int e = st.e0; e < st.e1; ++e) {
     double t[D];
 #pragma unroll
@@ -226,6 +395,52 @@ __global__ void __launch_bounds__(kRowT) classed_rows_kernel(RowClasses L, P p) 
     for (int k = 0; k < D; ++k) st.acc[k] = st.acc[k] + t[k];
   }
   p.finish(st, true);
+}
+
+// Side stream + events for running the heavy rows beside the tiles.
+struct RowStreams {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  RowStreams() = default;
+  RowStreams(const RowStreams&) = delete;
+  RowStreams& operator=(const RowStreams&) = delete;
+  ~RowStreams() {
+    if (side) {
+      (void)hipStreamSynchronize(side);
+      (void)hipStreamDestroy(side);
+    }
+    if (fork) (void)hipEventDestroy(fork);
+    if (join) (void)hipEventDestroy(join);
+  }
+  void ensure() {
+    if (side) return;
+    GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    GE_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    GE_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  }
+};
+
+// All rows of `rc` on stream s (the heavy ones on rs.side when there are tiles;
+// s waits for them before returning to the caller's next work).
+template <int D, class P>
+inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
+  const int tgrid = rc.ntiles;
+  if (rc.ntiles > 0 && rc.nheavy > 0 && std::getenv("GE_ROWS_SERIAL")) {  // tuning: no overlap
+    hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.nheavy), dim3(kRowT), 0, s, rc, p);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);
+  } else if (rc.ntiles > 0 && rc.nheavy > 0) {
+    rs.ensure();
+    GE_HIP(hipEventRecord(rs.fork, s));
+    GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+    hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.nheavy), dim3(kRowT), 0, rs.side, rc, p);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);
+    GE_HIP(hipEventRecord(rs.join, rs.side));
+    GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
+  } else if (rc.ntiles > 0) {
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);
+  } else if (rc.grid() > 0) {
+    hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.grid()), dim3(kRowT), 0, s, rc, p);
+  }
 }
 
 }  // namespace ge

@@ -22,7 +22,8 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libge.so")
+# GE_LIB_PATH: a variant build of the same library (kernel tuning scripts only)
+LIB_PATH = os.environ.get("GE_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libge.so")
 HEADER = os.path.join(REPO_ROOT, "include", "ge.h")
 
 MODE_STRICT = 0

@@ -132,3 +132,24 @@ def with_hubs(A, hubs, seed=0):
         src.append(np.full(k, h))
         dst.append(nb)
     return csr_from_edges(n, np.concatenate(src), np.concatenate(dst))
+
+
+def with_degrees(A, targets, seed=0):
+    """A plus edges so that vertex v has exactly targets[v] neighbours (each
+    added edge goes to a random non-neighbour; unit weights, symmetric).
+    Targets are applied in order; a later star may raise an earlier vertex's
+    degree by one, so keep target vertices apart from each other's stars."""
+    n = len(A[0]) - 1
+    rs = np.random.RandomState(seed)
+    src = np.repeat(np.arange(n), np.diff(A[0])).astype(np.int64)
+    dst = A[1].astype(np.int64)
+    protect = np.array(list(targets.keys()))
+    for v, k in targets.items():
+        nbrs = set(dst[src == v].tolist())
+        need = k - len(nbrs)
+        assert need >= 0, (v, k, len(nbrs))
+        pool = np.setdiff1d(np.arange(n), np.concatenate([[v], list(nbrs), protect]))
+        nb = rs.choice(pool, size=need, replace=False)
+        src = np.concatenate([src, np.full(need, v), nb])
+        dst = np.concatenate([dst, nb, np.full(need, v)])
+    return csr_from_edges(n, src, dst)

@@ -64,10 +64,13 @@ def test_fa_tiled_kernel_bitexact(ctx, oracle, n, dim):
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=5), want)
 
 
+@pytest.mark.parametrize("tiles", ["0", "1"])
 @pytest.mark.parametrize("use_weights", [1, 0])
-def test_fa_degree_classes(ctx, oracle, use_weights):
+def test_fa_degree_classes(ctx, oracle, monkeypatch, use_weights, tiles):
     """Rows of every degree class of the attraction kernel (ge_rows.hpp): light,
-    wave-per-row (> 32 edges) and block-per-row (> 2048 edges, several chunks)."""
+    wave-per-row (> 32 edges) and block-per-row (> 2048 edges, several chunks);
+    with GE_ROWS_TILES=1 the tiles (<= 1024 entries) and block-per-row beyond."""
+    monkeypatch.setenv("GE_ROWS_TILES", tiles)
     A = G.with_hubs(G.rmat(6000, 30000, seed=11), [(5, 4500), (17, 2100), (900, 300)])
     A = (A[0], A[1], np.random.RandomState(2).uniform(0.5, 2.0, len(A[1])))
     deg = np.diff(A[0])
@@ -76,6 +79,21 @@ def test_fa_degree_classes(ctx, oracle, use_weights):
     want = oracle.force_atlas(A, 3, coords=X0, iterations=4, use_weights=use_weights)
     got = ctx.force_atlas(A, 3, coords=X0, iterations=4, use_weights=use_weights)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("dim", [1, 2, 3, 4])
+def test_fa_row_tiles(ctx, oracle, monkeypatch, dim):
+    """Tiled CSR rows: rows at and around the tile capacity (1023-1025 entries:
+    tile vs block-per-row), tiles closed by the row limit (128 rows) and by the
+    entry limit, isolated rows, every dimension."""
+    monkeypatch.setenv("GE_ROWS_TILES", "1")
+    A = G.with_degrees(G.rmat(5000, 20000, seed=dim), {7: 1023, 8: 1024, 9: 1025, 300: 700,
+                                                       301: 400, 4000: 1500}, seed=dim)
+    deg = np.diff(A[0])
+    assert list(deg[[7, 8, 9, 300]]) == [1023, 1024, 1025, 700] and (deg == 0).any()
+    X0 = G.random_coords(len(deg), dim, seed=dim)
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=3)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=3), want)
 
 
 @pytest.mark.parametrize("R", ["1", "2", "4", "8"])
@@ -237,10 +255,13 @@ def test_faml_size_classes(ctx, oracle, sizes):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("R,U", [(1, 1), (1, 2), (1, 4), (2, 1), (4, 1)])
-def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U):
+@pytest.mark.parametrize("R,U,tiles", [(1, 1, "0"), (1, 1, "1"), (1, 2, "1"), (1, 4, "0"),
+                                        (2, 1, "1"), (4, 1, "0")])
+def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles):
     """Streamed path (faml_big_repulse / faml_big_edges) with 1, 2 and 4 row
-    slots per lane, ragged last items, and hub rows longer than one 64-edge chunk."""
+    slots per lane, ragged last items, and hub rows longer than one 64-edge chunk;
+    member rows tiled or classed (GE_ROWS_TILES)."""
+    monkeypatch.setenv("GE_ROWS_TILES", tiles)
     monkeypatch.setenv("GE_FAML_R", str(R))
     monkeypatch.setenv("GE_FAML_U", str(U))
     sizes = [3000, 700, 2203, 90, 1]
