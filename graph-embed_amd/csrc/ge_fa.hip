@@ -413,37 +413,79 @@ __device__ __forceinline__ void group_add(const double (&t)[U][D], int tid, int 
   wave_lds_sync();
 }
 
-// Software-pipelined ordered group sum for the domain-only kernel: the terms
-// of chunk c+1 are evaluated while the sums of chunk c are formed, in one
-// branch-free block (every lane of a group adds its group's terms; all end
-// with the same acc).  term(q, t) writes the term of chunk-local item q.
-// tb holds two chunk buffers of T*D doubles.
+// a += p[0] + ... + p[cnt-1] in order for a chunk of G slots (p 16-byte
+// aligned; slots >= cnt are added as +0.0, which leaves a unchanged: a running
+// sum is never -0).  Branch-free, so the reads of a batch issue together.
+template <int G>
+__device__ __forceinline__ double group_chain(double a, const double* p, int cnt) {
+  constexpr int B = G < 16 ? G : 16;  // terms per batch of reads
+#pragma unroll
+  for (int b0 = 0; b0 < G; b0 += B) {
+    double v[B];
+#pragma unroll
+    for (int l = 0; l < B; l += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(p + b0 + l);
+      v[l] = x.x;
+      v[l + 1] = x.y;
+    }
+#pragma unroll
+    for (int l = 0; l < B; ++l) a = a + ((b0 + l < cnt) ? v[l] : 0.0);
+  }
+  return a;
+}
+
+// Software-pipelined ordered group sum for the domain-only kernels: the terms
+// of chunk c+1 are evaluated while the sums of chunk c are formed.  Lane k (< D)
+// of a group carries dimension k's running sum (one dependent add per term);
+// the group's terms sit dimension-major in its region of the chunk buffer
+// (groups smaller than D: every lane adds every dimension).  All lanes of a
+// group end with the full acc.  term(q, t) writes the term of
+// chunk-local item q.  tb holds two chunk buffers of T*D doubles (16-byte
+// aligned); G >= 2.
 template <int D, int G, int T, class Term>
 __device__ __forceinline__ void pipelined_group_sum(int nitems, int tid, int g, double* tb,
                                                     Term&& term, double (&acc)[D]) {
+  static_assert(G <= 64, "a group lives in one wave");
   if (nitems <= 0) return;
+  if constexpr (G == 1) {  // (callers take other paths for G == 1)
+    for (int q = 0; q < nitems; ++q) {
+      double t[D];
+      term(q, t);
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[k];
+    }
+    return;
+  }
   const int base = tid - g;
+  // G >= D: lane k carries dimension k; smaller groups: every lane all of them
+  constexpr bool kLaneDim = G >= D;
+  const int kd = g < D ? g : D - 1;
+  double a = lane_dim_value<D>(acc, kd);
   double t[D];
   term(g, t);  // chunk 0
 #pragma unroll
-  for (int k = 0; k < D; ++k) tb[tid * D + k] = t[k];
+  for (int k = 0; k < D; ++k) tb[base * D + k * G + g] = t[k];
   for (int c0 = 0; c0 < nitems; c0 += G) {
     const int cur = (c0 / G) & 1;
     wave_lds_sync();
     const bool more = c0 + G < nitems;
     if (more) term(c0 + G + g, t);  // next chunk, independent of the adds below
+    const double* reg = tb + cur * T * D + base * D;
     const int cnt = min(G, nitems - c0);
-    const double* src = tb + cur * T * D + base * D;
+    if constexpr (kLaneDim) {
+      a = group_chain<G>(a, reg + kd * G, cnt);
+    } else {
 #pragma unroll
-    for (int l = 0; l < G; ++l)
-      if (l < cnt)
-#pragma unroll
-        for (int k = 0; k < D; ++k) acc[k] = acc[k] + src[l * D + k];
+      for (int k = 0; k < D; ++k) acc[k] = group_chain<G>(acc[k], reg + k * G, cnt);
+    }
     wave_lds_sync();
     if (more)
 #pragma unroll
-      for (int k = 0; k < D; ++k) tb[((cur ^ 1) * T + tid) * D + k] = t[k];
+      for (int k = 0; k < D; ++k) tb[(cur ^ 1) * T * D + base * D + k * G + g] = t[k];
   }
+  if constexpr (kLaneDim)
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = __shfl(a, (base & 63) + k);
 }
 
 // STAGED: the CSR indices and weights (nnz <= kSmallNnz) are copied to LDS once.
@@ -462,7 +504,7 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
   constexpr int W = Rec<D>::W;
   constexpr int U = 1;
   __shared__ __attribute__((aligned(16))) double sx[kSmallMax * W];
-  __shared__ double tb[(G > 1 ? T * U * (DOMAIN_ONLY ? 2 : 1) : 1) * D];
+  __shared__ __attribute__((aligned(16))) double tb[(G > 1 ? T * U * (DOMAIN_ONLY ? 2 : 1) : 1) * D];
   __shared__ int s_ix[STAGED ? small_nnz_cap(D) : 1];
   __shared__ double s_dx[STAGED ? small_nnz_cap(D) : 1];
   const int it0 = DOMAIN_ONLY ? 0 : *it_state;
@@ -775,6 +817,105 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
     for (int k = 0; k < D; ++k) Frep[(size_t)(i - rb) * D + k] = acc[k];
 }
 
+// One whole iteration of a small level (n <= grouped_cap) in one launch: the
+// repulsion group sum, then the CSR row's attraction terms (neighbours from the
+// LDS records) continuing the same ordered sum, then gravity, swing and the
+// update (:146-269).  Rows [rb, re); Fprev indexed by row - rb.  LINEAR: the
+// caller guarantees linlog == 0 and delta == 1 (the in-domain bodies use it).
+template <int D, int G, bool REPEL_ONE, bool LINEAR>
+__global__ void __launch_bounds__(kGrpT)
+fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
+                const double* __restrict__ dx, const double* __restrict__ X,
+                const double* __restrict__ dp1, FaConst c, double* __restrict__ Fprev,
+                double* __restrict__ Xnext) {
+  constexpr int W = Rec<D>::W;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* rec = smem;
+  double* tb = smem + (size_t)n * W;
+  const int tid = threadIdx.x;
+  const int g = tid % G;
+  const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
+  const bool active = i < re;
+  bool ok = REPEL_ONE || weight_ok(c.repel);
+  for (int q = tid; q < n; q += kGrpT) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const double v = X[(size_t)q * D + k];
+      rec[q * W + k] = v;
+      ok = ok && coord_ok(v);
+    }
+    const double w = dp1[q];
+    rec[q * W + D] = w;
+    ok = ok && weight_ok(w);
+  }
+  double xi[D], acc[D], fprev[D];
+  const int e0 = active ? ip[i] : 0;
+  const int e1 = active ? ip[i + 1] : 0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) fprev[k] = (active && g == 0) ? Fprev[(size_t)(i - rb) * D + k] : 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xi[k] = active ? rec[i * W + k] : 0.0;
+    acc[k] = 0.0;
+  }
+  const double di = active ? rec[i * W + D] : 1.0;
+  if (__syncthreads_and(ok) && G > 1) {  // block-uniform: every record in the domain
+    pipelined_group_sum<D, G, kGrpT>(n, tid, g, tb, [&](int q, double (&t)[D]) {
+      const int jj = min(q, n - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[k] = 0.0;
+      rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
+      if (q >= n)
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+    }, acc);
+    pipelined_group_sum<D, G, kGrpT>(e1 - e0, tid, g, tb, [&](int q, double (&t)[D]) {
+      const int ee = min(e0 + q, e1 - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[k] = 0.0;
+      attr_edge<D, true, LINEAR>(xi, &rec[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, di, c, t);
+      if (e0 + q >= e1)
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+    }, acc);
+  } else {
+    const bool row_ok = vertex_ok<D>(xi, di) && (REPEL_ONE || weight_ok(c.repel));
+    for (int j0 = 0; j0 < n; j0 += G) {  // :151-167, j ascending
+      double t[1][D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[0][k] = 0.0;
+      const int j = j0 + g;
+      if (active && j < n) {
+        const double* xj = &rec[j * W];
+        if (row_ok && vertex_ok<D>(xj, rec[j * W + D]))
+          rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+        else
+          rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+      }
+      group_add<D, G, 1>(t, tid, g, min(G, n - j0), active && g == 0, tb, acc);
+    }
+    const bool xi_ok = all_coord_ok<D>(xi);
+    for (int b = 0; b < e1 - e0; b += G) {  // :169-203, CSR order
+      double t[1][D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[0][k] = 0.0;
+      const int e = e0 + b + g;
+      if (e < e1) {
+        const double* xj = &rec[ix[e] * W];
+        const double a = c.use_weights ? dx[e] : 1.0;
+        if (xi_ok && all_coord_ok<D>(xj))
+          attr_edge<D, true>(xi, xj, a, di, c, t[0]);
+        else
+          attr_edge<D, false>(xi, xj, a, di, c, t[0]);
+      }
+      group_add<D, G, 1>(t, tid, g, min(G, e1 - e0 - b), active && g == 0, tb, acc);
+    }
+  }
+  if (active && g == 0)
+    finish_row<D>(i, i - rb, xi, acc, fprev, di, c, Fprev, Xnext, true);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launch helpers
 
@@ -785,6 +926,17 @@ int device_cus() {
   GE_HIP(hipGetDevice(&dev));
   GE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   return cus > 0 ? cus : 256;
+}
+
+// Lanes per row of the small-level kernels.
+inline int grouped_lanes(int rows) {
+  int G = 1;  // lanes per row: aim for >= 64 K threads, at most one wave per row
+  while (G < 64 && (long long)rows * G < 65536) G *= 2;
+  if (const char* e = std::getenv("GE_GRP_G")) {  // tuning / test override
+    const int g = std::atoi(e);
+    if (g >= 1 && g <= 64 && (g & (g - 1)) == 0) G = g;
+  }
+  return G;
 }
 
 template <int D>
@@ -804,13 +956,7 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
     return;
   }
   if (n <= grouped_cap(D)) {
-    // lanes per row: aim for >= 64 K threads, at most one wave per row
-    int G = 1;
-    while (G < 64 && (long long)rows * G < 65536) G *= 2;
-    if (const char* e = std::getenv("GE_GRP_G")) {  // tuning / test override
-      const int g = std::atoi(e);
-      if (g >= 1 && g <= 64 && (g & (g - 1)) == 0) G = g;
-    }
+    const int G = grouped_lanes(rows);
     auto go = [&](auto GG) {
       constexpr int GC = decltype(GG)::value;
       const int nb = (rows + kGrpT / GC - 1) / (kGrpT / GC);
@@ -864,6 +1010,48 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
                          rb, re, per, X, dp1, repel, Frep);
   };
   switch (R) {
+    case 8: go(std::integral_constant<int, 8>()); break;
+    case 4: go(std::integral_constant<int, 4>()); break;
+    case 2: go(std::integral_constant<int, 2>()); break;
+    default: go(std::integral_constant<int, 1>()); break;
+  }
+}
+
+// Small levels (n <= grouped_cap): fa_grouped_step, one launch per iteration.
+template <int D>
+void launch_grouped_step(hipStream_t s, int n, int rb, int re, const int* ip, const int* ix,
+                         const double* dx, const double* X, const double* dp1, const FaConst& c,
+                         double* Fprev, double* Xnext) {
+  const int rows = re - rb;
+  if (rows <= 0) return;
+  const size_t lds = grouped_lds_bytes(n, D);
+  auto go = [&](auto GG) {
+    constexpr int GC = decltype(GG)::value;
+    const int nb = (rows + kGrpT / GC - 1) / (kGrpT / GC);
+    auto one = [&](auto RO, auto LI) {
+      constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
+      if (lds > 65536)  // above the default dynamic-LDS limit
+        GE_HIP(hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&fa_grouped_step<D, GC, R1, LIN>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL((fa_grouped_step<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s, n, rb,
+                         re, ip, ix, dx, X, dp1, c, Fprev, Xnext);
+    };
+    const bool lin = !c.linlog && c.delta == 1.0;
+    using T = std::true_type;
+    using F = std::false_type;
+    if (c.repel == 1.0) {
+      if (lin) one(T(), T());
+      else one(T(), F());
+    } else {
+      if (lin) one(F(), T());
+      else one(F(), F());
+    }
+  };
+  switch (grouped_lanes(rows)) {
+    case 64: go(std::integral_constant<int, 64>()); break;
+    case 32: go(std::integral_constant<int, 32>()); break;
+    case 16: go(std::integral_constant<int, 16>()); break;
     case 8: go(std::integral_constant<int, 8>()); break;
     case 4: go(std::integral_constant<int, 4>()); break;
     case 2: go(std::integral_constant<int, 2>()); break;
@@ -953,6 +1141,12 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   }
   dispatch_dim(pl->dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
+    if (pl->p.mode == GE_MODE_STRICT && pl->n <= grouped_cap(D) && !std::getenv("GE_GRP_SPLIT")) {
+      launch_grouped_step<D>(s, pl->n, pl->rb, pl->re, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p,
+                             pl->c, pl->fprev.p, xn);
+      if (ev) GE_HIP(hipEventRecord(ev[1], s));
+      return;
+    }
     launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
                         pl->frep.p, pl->fpart.p, pl->cus);
     if (ev) GE_HIP(hipEventRecord(ev[1], s));

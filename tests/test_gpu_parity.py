@@ -136,15 +136,28 @@ def test_fa_small_kernel_out_of_domain_start(ctx, oracle, monkeypatch, small_max
     assert np.array_equal(ctx.force_atlas(A, 2, coords=X0, iterations=25), want)
 
 
-@pytest.mark.parametrize("grp", ["1", "4", "16", "64"])
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("grp", ["1", "2", "4", "16", "64"])
 @pytest.mark.parametrize("n,dim", [(700, 3), (1400, 4), (2900, 2)])
-def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim):
-    """Small-n repulsion (fa_repulse_grouped): G lanes per row, in-order group sums."""
+def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim, split):
+    """Small levels: G lanes per row, in-order group sums; one fused launch per
+    iteration (fa_grouped_step) or repulsion + row kernels (GE_GRP_SPLIT=1)."""
     monkeypatch.setenv("GE_GRP_G", grp)
+    if split == "1":
+        monkeypatch.setenv("GE_GRP_SPLIT", "1")
     A = G.rmat(n, 6 * n, seed=n)
     X0 = G.random_coords(n, dim, seed=int(grp))
     want = oracle.force_atlas(A, dim, coords=X0, iterations=4)
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=4), want)
+
+
+def test_fa_small_level_graph_replay(ctx, oracle):
+    """n = 127-ish coarsest level (fused grouped kernel, 64 lanes per row) over
+    3000 iterations: captured-graph replay of the fused step, bit-exact."""
+    A = G.largest_component(G.rmat(160, 700, seed=9))
+    assert 64 < len(A[0]) - 1 <= 3072
+    want = oracle.force_atlas(A, 3, iterations=3000, seed=77)
+    assert np.array_equal(ctx.force_atlas(A, 3, iterations=3000, seed=77), want)
 
 
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
