@@ -96,6 +96,16 @@ def test_fa_row_tiles(ctx, oracle, monkeypatch, dim):
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=3), want)
 
 
+def test_fa_row_tiles_graph_replay(ctx, oracle, monkeypatch):
+    """Tiles + heavy rows on the side stream inside a captured graph (>= 128
+    iterations replay 32-iteration graphs with the fork/join events)."""
+    monkeypatch.setenv("GE_ROWS_TILES", "1")
+    A = G.with_degrees(G.rmat(3300, 12000, seed=21), {5: 1500, 6: 900}, seed=2)
+    X0 = G.random_coords(3300, 2, seed=6)
+    want = oracle.force_atlas(A, 2, coords=X0, iterations=130)
+    assert np.array_equal(ctx.force_atlas(A, 2, coords=X0, iterations=130), want)
+
+
 @pytest.mark.parametrize("R", ["1", "2", "4", "8"])
 def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
     """fa_repulse_strict with R row slots x 8/R partners in flight per lane
