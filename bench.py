@@ -69,7 +69,8 @@ def log(rank, *a):
 
 
 def pmc_traffic_per_launch(kernel_prefix, workload):
-    """HBM bytes per launch of a kernel from the committed rocprofv3 PMC passes of
+    """HBM bytes per step of the kernels whose names contain kernel_prefix (summed
+    over distinct kernels, averaged over launches) from the committed rocprofv3 PMC passes of
     the same workload (profiles/*/pmc_fetch_<workload>*.csv, pmc_write_<...>.csv).  gfx950 correction from
     MI355X_MICROARCH.md: FETCH_SIZE reports half the bytes of a wide coalesced
     read -> bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024."""
@@ -77,14 +78,14 @@ def pmc_traffic_per_launch(kernel_prefix, workload):
         import csv
         # newest round directory first; the first file that traced this kernel wins
         for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", pattern)), reverse=True):
-            vals = []
+            vals = {}  # per kernel name (one step may launch several matching kernels)
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    if row.get("Counter_Name") == counter and row.get("Kernel_Name", "").find(
-                            kernel_prefix) >= 0:
-                        vals.append(float(row["Counter_Value"]))
+                    name = row.get("Kernel_Name", "")
+                    if row.get("Counter_Name") == counter and name.find(kernel_prefix) >= 0:
+                        vals.setdefault(name, []).append(float(row["Counter_Value"]))
             if vals:
-                return sum(vals) / len(vals), path
+                return sum(sum(v) / len(v) for v in vals.values()), path
         return None
     f = read(f"pmc_fetch_{workload}*.csv", "FETCH_SIZE")
     w = read(f"pmc_write_{workload}*.csv", "WRITE_SIZE")
@@ -469,7 +470,8 @@ def main():
             "launches": launches,
         },
         "roofline_attraction": {
-            "kernel": "classed_rows_kernel<FaRows> (CSR attraction + gravity + update)",
+            "kernel": "tile_rows_kernel<FaRows> + classed_rows_kernel<FaRows> on a side stream "
+                      "(CSR attraction + gravity + update; time = both, fork to join)",
             "bound": "hbm",
             "achieved": att_gbs,
             "peak": HBM_PEAK_GBS,

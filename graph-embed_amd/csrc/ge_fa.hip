@@ -1112,10 +1112,13 @@ static void plan_init(ge_fa_plan* pl) {
       ids[q] = pl->rb + q;
       deg[q] = h_ip[q + 1] - h_ip[q];
     }
-    classify_rows(ids, deg, order, pl->rc);
+    // single level: a row's sum starts at its repulsion over all n vertices, far
+    // above the edge terms, so heavy rows split into binade-sum segments
+    classify_rows(ids, deg, order, pl->rc, true);
     pl->rows.alloc(order.size());
     pl->rows.upload(order.data(), order.size(), s);
     pl->rc.bind(pl->rows.p);
+    pl->rstreams.attach(pl->rc, pl->dim, s);
     GE_HIP(hipStreamSynchronize(s));
   }
   hipLaunchKernelGGL(degp1_kernel, dim3((pl->n + 255) / 256), dim3(256), 0, s, pl->n, pl->ip,

@@ -759,11 +759,14 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       const int v = h_ptix[rows[q]];
       deg[q] = h_ip[v + 1] - h_ip[v];
     }
-    classify_rows(rows, deg, erows, pl->ecls);
+    // the in-aggregate repulsion is not far above the external pulls (measured
+    // at C3: every heavy row left the binade), so heavy rows stay whole
+    classify_rows(rows, deg, erows, pl->ecls, false);
     pl->ecode.alloc(std::max(h_ip[pl->n], 1));
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
     pl->ecls.bind(pl->erows.p);
+    pl->rstreams.attach(pl->ecls, pl->dim, st);
   }
   struct Item { int a, r0; double work; };
   std::vector<Item> its;

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -55,20 +56,28 @@ constexpr int kTileMinRows = 65536;  // fewer rows: medium / light classes
 struct RowClasses {
   const int* rows = nullptr;
   const int* tile_ptr = nullptr;  // ntiles + 1 offsets into rows
-  int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0;
+  const int* seg = nullptr;       // nseg x {heavy row slot, first, last entry offset in the row}
+  long long* hacc = nullptr;      // nheavy x D x {S, A}: binade sums of the segments (zeroed)
+  int* hflag = nullptr;           // nheavy: a segment could not use the binade sum
+  int* nfall = nullptr;           // count of heavy-row passes summed serially (GE_ROWS_STATS)
+  int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0, nseg = 0;
   int tile_off = 0;  // where tile_ptr starts in the host array
+  int seg_off = 0;   // where seg starts in the host array
   int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
   void bind(const int* dev) {
     rows = dev;
     tile_ptr = dev + tile_off;
+    seg = dev + seg_off;
   }
 };
 
 // Host: order `ids` (row ids with their degrees) into classes; `out` gets the
 // row list followed by the tile boundaries (upload all of it, then bind()).
 // GE_ROWS_MED / GE_ROWS_HEAVY / GE_ROWS_TILES override the choices (tuning).
+// segments: heavy rows may be split into binade-sum segments (the policy's
+// row sums start far above its edge terms: single-level forceAtlas).
 inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
-                          std::vector<int>& out, RowClasses& rc) {
+                          std::vector<int>& out, RowClasses& rc, bool segments) {
   bool tiles = ids.size() >= (size_t)kTileMinRows;
   if (const char* e = std::getenv("GE_ROWS_TILES")) tiles = std::atoi(e) != 0;
   // few rows (a small level): latency, not throughput -- rows of more than 4
@@ -107,6 +116,25 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
   }
   rc.tile_off = (int)out.size();
   out.insert(out.end(), tp.begin(), tp.end());
+  // heavy rows as segments of <= kTileCap entries (tile mode; GE_ROWS_SEGMENTS=0: whole rows
+  // on a side stream instead)
+  bool segs = tiles && segments;
+  if (const char* e = std::getenv("GE_ROWS_SEGMENTS")) segs = segs && std::atoi(e) != 0;
+  rc.seg_off = (int)out.size();
+  rc.nseg = 0;
+  if (segs) {
+    int h = 0;
+    for (size_t q = 0; q < ids.size(); ++q) {
+      if (deg[q] <= heavy) continue;
+      for (int a = 0; a < deg[q]; a += kTileCap) {
+        out.push_back(h);
+        out.push_back(a);
+        out.push_back(std::min(deg[q], a + kTileCap));
+        ++rc.nseg;
+      }
+      ++h;
+    }
+  }
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -258,6 +286,58 @@ __device__ __forceinline__ double lane_chain_any(double a, const double* p, int 
   return a;
 }
 
+// ---------------------------------------------------------------------------
+// Exact ordered sums without the serial chain (heavy rows).
+//
+// A row's sum starts at s0 = its repulsion force (a normal double, usually far
+// larger than the edge terms) and adds the terms in stored order, rounding each
+// step to nearest.  Let u = ulp(s0) = 2^(e-52) and P0 = s0/u, an integer with
+// 2^52 <= |P0| < 2^53.  If the running value stays in s0's binade, every
+// representable number there is a multiple of u, so each step rounds the exact
+// Q*u + t to (Q + rint(t/u))*u -- unless t/u is a half-integer (a tie, decided
+// by Q's parity).  Hence, with r_i = rint(t_i/u), no ties and every prefix
+// P0 + r_1 + ... + r_k strictly inside (2^52, 2^53) in magnitude, the serial
+// result is (P0 + sum r_i)*u bit for bit: integer sums, so any order and any
+// split of the row gives it.  |prefix - P0| <= A = sum |r_i|, so
+// 2^52 < |P0| - A and |P0| + A < 2^53 covers every prefix.  Segments of a heavy
+// row accumulate S = sum r_i and A in int64 (|r_i| < 2^36 or the row is
+// flagged); rows that fail any test (s0 zero/subnormal/non-finite, a tie, a
+// large term, a binade crossing) are summed serially in stored order instead.
+constexpr double kBinadeMagic = 0x1.8p52;  // f + M rounds f (|f| < 2^51) to an integer
+constexpr double kBinadeBig = 0x1p36;
+
+__device__ __forceinline__ bool binade_base(double s0, int& uexp, long long& P0) {
+  const long long b = __double_as_longlong(s0);
+  const int ex = (int)((b >> 52) & 0x7ff);
+  if (ex == 0 || ex == 0x7ff) return false;  // zero, subnormal, inf, nan
+  uexp = ex - 1023 - 52;
+  P0 = (b & ((1ll << 52) - 1)) | (1ll << 52);  // |s0| / u
+  if (b < 0) P0 = -P0;
+  return true;
+}
+
+// rint(t / 2^uexp) as an integer; flag on a tie or |t / 2^uexp| >= 2^36 (or nan)
+__device__ __forceinline__ long long binade_term(double t, int uexp, int& flag) {
+  const double f = ldexp(t, -uexp);  // exact unless |f| < 2^-1022 (then rint(f) = 0)
+  if (!(fabs(f) < kBinadeBig)) {
+    flag = 1;
+    return 0;
+  }
+  const double y = f + kBinadeMagic;  // round to nearest even integer
+  const double r = y - kBinadeMagic;
+  if (fabs(f - r) == 0.5) flag = 1;  // exact difference; a tie depends on the parity of Q
+  return __double_as_longlong(y) - __double_as_longlong(kBinadeMagic);
+}
+
+// (P0 + S) * u when every prefix stays in the binade, else false
+__device__ __forceinline__ bool binade_result(long long P0, int uexp, long long S, long long A,
+                                              double& out) {
+  const long long m = P0 < 0 ? -P0 : P0;
+  if (!(m - A > (1ll << 52) && m + A < (1ll << 53))) return false;
+  out = ldexp((double)(P0 + S), uexp);  // |P0 + S| < 2^53: exact
+  return true;
+}
+
 // LDS bytes of the classed kernel (heavy / medium rows) and of a tile.
 template <int D, class P>
 struct RowsLds {
@@ -344,12 +424,114 @@ __device__ __forceinline__ void tile_rows(const RowClasses& L, const P& p, int t
   }
 }
 
+// One segment of a heavy row (entries [a, b) of it, b - a <= kTileCap): the
+// binade sums of its terms, added to the row's accumulators.
+template <int D, class P>
+__device__ __forceinline__ void segment_rows(const RowClasses& L, const P& p, int q, char* lds) {
+  using State = typename P::State;
+  long long* red = reinterpret_cast<long long*>(lds);  // [4 waves][2D]
+  int* rflag = reinterpret_cast<int*>(lds + sizeof(long long) * 4 * 2 * D);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int h = L.seg[3 * q], a = L.seg[3 * q + 1], b = L.seg[3 * q + 2];
+  State st;
+  p.load(L.rows[h], st);
+  int uexp[D];
+  long long P0[D], S[D], A[D];
+  int flag = 0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    if (!binade_base(st.acc[k], uexp[k], P0[k])) flag = 1;
+    S[k] = A[k] = 0;
+  }
+  if (!flag) {
+    constexpr int U = kTileCap / kRowT;
+    double tt[U][D];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = st.e0 + min(a + tid + kRowT * u, b - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) tt[u][k] = 0.0;
+      p.term(st, e, tt[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (a + tid + kRowT * u < b)
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const long long r = binade_term(tt[u][k], uexp[k], flag);
+          S[k] += r;
+          A[k] += r < 0 ? -r : r;
+        }
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      S[k] += __shfl_xor(S[k], o);
+      A[k] += __shfl_xor(A[k], o);
+    }
+  const bool any = __any(flag);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      red[wv * 2 * D + 2 * k] = S[k];
+      red[wv * 2 * D + 2 * k + 1] = A[k];
+    }
+    rflag[wv] = any ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid < 2 * D) {
+    const long long v = red[tid] + red[2 * D + tid] + red[4 * D + tid] + red[6 * D + tid];
+    atomicAdd(reinterpret_cast<unsigned long long*>(L.hacc + (size_t)h * 2 * D + tid),
+              (unsigned long long)v);
+  }
+  if (tid == 0 && (rflag[0] | rflag[1] | rflag[2] | rflag[3])) atomicOr(L.hflag + h, 1);
+}
+
+// After every segment: one wave per heavy row turns its binade sums into the
+// row's force (or, when they do not apply, adds its terms serially in stored
+// order), then gravity and the update; the accumulators are zeroed for the
+// next pass.
+template <int D, class P>
+__global__ void __launch_bounds__(kRowT) heavy_finish_kernel(RowClasses L, P p) {
+  __shared__ __attribute__((aligned(16))) double buf[4 * 64 * D];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int h = blockIdx.x * 4 + (tid >> 6);
+  if (h >= L.nheavy) return;  // wave-uniform
+  typename P::State st;
+  p.load(L.rows[h], st);
+  long long* acc = L.hacc + (size_t)h * 2 * D;
+  bool ok = L.hflag[h] == 0;
+  double sum[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    int uexp;
+    long long P0;
+    ok = ok && binade_base(st.acc[k], uexp, P0) && binade_result(P0, uexp, acc[2 * k], acc[2 * k + 1], sum[k]);
+  }
+  if (ok) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) st.acc[k] = sum[k];
+  } else {
+    if (lane == 0 && L.nfall) atomicAdd(L.nfall, 1);
+    ordered_edge_sum<D, 1>(st.e0, st.e1, lane, buf + (tid >> 6) * 64 * D,
+                           [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
+  }
+  p.finish(st, lane == 0);
+  wave_lds_sync();  // every lane has read the accumulators
+  if (lane < 2 * D) acc[lane] = 0;
+  if (lane == 0) L.hflag[h] = 0;
+}
+
 // Tiles get their own kernel: without the heavy path's registers and LDS it
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
 template <int D, class P>
 __global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
-  tile_rows<D>(L, p, blockIdx.x, lds);
+  if ((int)blockIdx.x < L.ntiles)
+    tile_rows<D>(L, p, blockIdx.x, lds);
+  else
+    segment_rows<D>(L, p, blockIdx.x - L.ntiles, lds);
 }
 
 // P: a row policy with
@@ -397,14 +579,39 @@ __global__ void __launch_bounds__(kRowT, GE_ROWS_MINBLOCKS) classed_rows_kernel(
   p.finish(st, true);
 }
 
-// Side stream + events for running the heavy rows beside the tiles.
+// Per-plan row resources: the side stream + events for running whole heavy rows
+// beside the tiles, and the heavy rows' binade accumulators (segment mode).
 struct RowStreams {
+  DevBuf<long long> hacc;
+  DevBuf<int> hflag, nfall;
+  int nheavy = 0;
+  // allocate and zero the accumulators of rc's heavy rows (segment mode)
+  void attach(RowClasses& rc, int D, hipStream_t s) {
+    if (rc.nseg == 0) return;
+    hacc.alloc((size_t)rc.nheavy * 2 * D);
+    hflag.alloc(rc.nheavy);
+    GE_HIP(hipMemsetAsync(hacc.p, 0, sizeof(long long) * hacc.n, s));
+    GE_HIP(hipMemsetAsync(hflag.p, 0, sizeof(int) * hflag.n, s));
+    rc.hacc = hacc.p;
+    rc.hflag = hflag.p;
+    nheavy = rc.nheavy;
+    if (std::getenv("GE_ROWS_STATS")) {
+      nfall.alloc(1);
+      GE_HIP(hipMemsetAsync(nfall.p, 0, sizeof(int), s));
+      rc.nfall = nfall.p;
+    }
+  }
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   RowStreams() = default;
   RowStreams(const RowStreams&) = delete;
   RowStreams& operator=(const RowStreams&) = delete;
   ~RowStreams() {
+    if (nfall.p) {
+      int v = 0;
+      if (hipMemcpy(&v, nfall.p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess)
+        std::fprintf(stderr, "rows: %d heavy rows, %d serial fallbacks in total\n", nheavy, v);
+    }
     if (side) {
       (void)hipStreamSynchronize(side);
       (void)hipStreamDestroy(side);
@@ -424,7 +631,13 @@ struct RowStreams {
 // s waits for them before returning to the caller's next work).
 template <int D, class P>
 inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
-  const int tgrid = rc.ntiles;
+  const int tgrid = rc.ntiles + rc.nseg;
+  if (rc.nseg > 0) {  // heavy rows as segments, then their finish
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);
+    hipLaunchKernelGGL((heavy_finish_kernel<D, P>), dim3((rc.nheavy + 3) / 4), dim3(kRowT), 0, s,
+                       rc, p);
+    return;
+  }
   if (rc.ntiles > 0 && rc.nheavy > 0 && std::getenv("GE_ROWS_SERIAL")) {  // tuning: no overlap
     hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.nheavy), dim3(kRowT), 0, s, rc, p);
     hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);

@@ -47,15 +47,18 @@ for name in os.environ.get("GE_TUNE_GRAPHS", "rmat,lattice").split(","):
              os.environ.get("GE_TUNE_ENVS", "").split(";")]
     cfgs = [(c, e) for c in cfgs for e in extra]
     for (tiles, med, heavy), env in cfgs:
-        for k in ("GE_ROWS_SERIAL", "GE_TILE_GRID"):
+        for k in ("GE_ROWS_SERIAL", "GE_TILE_GRID", "GE_ROWS_SEGMENTS"):
             os.environ.pop(k, None)
         os.environ.update(env)
         os.environ["GE_ROWS_TILES"] = str(tiles)
         os.environ["GE_ROWS_MED"] = str(med)
         os.environ["GE_ROWS_HEAVY"] = str(heavy)
         plan = ctx.fa_plan(n, len(A[1]), ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), 3, 0, n)
+        for _ in range(2):  # warm-up (code objects, caches)
+            plan.step(X.data_ptr(), Y.data_ptr())
+        ctx.sync()
         plan.set_profiling(True)
-        for _ in range(3):
+        for _ in range(5):
             plan.step(X.data_ptr(), Y.data_ptr())
         ctx.sync()
         _, att_ms, _ = plan.kernel_ms()

@@ -81,12 +81,14 @@ def test_fa_degree_classes(ctx, oracle, monkeypatch, use_weights, tiles):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("segments", ["1", "0"])
 @pytest.mark.parametrize("dim", [1, 2, 3, 4])
-def test_fa_row_tiles(ctx, oracle, monkeypatch, dim):
-    """Tiled CSR rows: rows at and around the tile capacity (1023-1025 entries:
-    tile vs block-per-row), tiles closed by the row limit (128 rows) and by the
-    entry limit, isolated rows, every dimension."""
+def test_fa_row_tiles(ctx, oracle, monkeypatch, dim, segments):
+    """Tiled CSR rows: rows at and around the tile capacity (tile vs heavy),
+    tiles closed by the row limit and by the entry limit, isolated rows, every
+    dimension; heavy rows as binade-sum segments or whole rows (GE_ROWS_SEGMENTS)."""
     monkeypatch.setenv("GE_ROWS_TILES", "1")
+    monkeypatch.setenv("GE_ROWS_SEGMENTS", segments)
     A = G.with_degrees(G.rmat(5000, 20000, seed=dim), {7: 1023, 8: 1024, 9: 1025, 300: 700,
                                                        301: 400, 4000: 1500}, seed=dim)
     deg = np.diff(A[0])
@@ -94,6 +96,23 @@ def test_fa_row_tiles(ctx, oracle, monkeypatch, dim):
     X0 = G.random_coords(len(deg), dim, seed=dim)
     want = oracle.force_atlas(A, dim, coords=X0, iterations=3)
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=3), want)
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e9, 1e-300])
+def test_fa_heavy_segments_binade_and_fallback(ctx, oracle, monkeypatch, scale):
+    """Heavy rows split into segments whose terms are summed as integers in the
+    binade of the repulsion sum.  Edge weights of 1e9 make the terms too large
+    for the binade (|t/ulp| >= 2^36) and 1e-300 pushes the weighted degrees (and
+    so the repulsion sums) towards the subnormal range: both fall back to the
+    serial in-order sum.  Bit-exact either way."""
+    monkeypatch.setenv("GE_ROWS_TILES", "1")
+    A = G.with_degrees(G.rmat(7000, 28000, seed=4), {3: 5000, 11: 2600, 12: 513}, seed=5)
+    A = (A[0], A[1], A[2] * scale)
+    X0 = G.random_coords(7000, 3, seed=9)
+    for it in (1, 3):
+        want = oracle.force_atlas(A, 3, coords=X0, iterations=it)
+        got = ctx.force_atlas(A, 3, coords=X0, iterations=it)
+        assert np.array_equal(got, want), it
 
 
 def test_fa_row_tiles_graph_replay(ctx, oracle, monkeypatch):
