@@ -428,8 +428,13 @@ __device__ __forceinline__ double group_chain(double a, const double* p, int cnt
       v[l] = x.x;
       v[l + 1] = x.y;
     }
+    if (cnt >= G) {  // full chunk (group-uniform): no masking
 #pragma unroll
-    for (int l = 0; l < B; ++l) a = a + ((b0 + l < cnt) ? v[l] : 0.0);
+      for (int l = 0; l < B; ++l) a = a + v[l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + ((b0 + l < cnt) ? v[l] : 0.0);
+    }
   }
   return a;
 }

@@ -150,11 +150,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 // 4 contiguous 16-byte reads.
 template <int D>
 __device__ __forceinline__ double lane_dim_value(const double (&acc)[D], int kd) {
-  double a = acc[0];
+  // bitwise blend: a select chain over acc[] is turned into a dynamically
+  // indexed (scratch) load by the compiler
+  long long a = __double_as_longlong(acc[0]);
 #pragma unroll
-  for (int k = 1; k < D; ++k)
-    if (kd == k) a = acc[k];
-  return a;
+  for (int k = 1; k < D; ++k) {
+    const long long m = -(long long)(kd == k);
+    a = (a & ~m) | (__double_as_longlong(acc[k]) & m);
+  }
+  return __longlong_as_double(a);
 }
 
 // a += p[0] + p[1] + ... + p[cnt-1], in order (p 16-byte aligned).  Software
