@@ -921,6 +921,125 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
     finish_row<D>(i, i - rb, xi, acc, fprev, di, c, Fprev, Xnext, true);
 }
 
+// Mid-size levels (grouped_cap < n <= kStreamMax): the same fused iteration
+// with the records streamed through LDS in tiles of kStreamTile (the in-domain
+// test per tile, the attraction's neighbours read from X), so a coarsest level
+// of a few thousand to tens of thousands of vertices keeps G lanes per row.
+constexpr int kStreamTile = 2048;
+constexpr int kStreamMax = 65536;
+// GE_STREAM_MAX overrides the bound (tuning / tests)
+inline int stream_max() {
+  if (const char* e = std::getenv("GE_STREAM_MAX")) return std::atoi(e);
+  return kStreamMax;
+}
+inline size_t stream_lds_bytes(int D) {
+  return sizeof(double) * ((size_t)kStreamTile * ((D + 1 <= 4) ? 4 : 8) + 2 * kGrpT * D);
+}
+
+template <int D, int G, bool REPEL_ONE, bool LINEAR>
+__global__ void __launch_bounds__(kGrpT)
+fa_grouped_stream(int n, int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
+                  const double* __restrict__ dx, const double* __restrict__ X,
+                  const double* __restrict__ dp1, FaConst c, double* __restrict__ Fprev,
+                  double* __restrict__ Xnext) {
+  constexpr int W = Rec<D>::W;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* rec = smem;
+  double* tb = smem + (size_t)kStreamTile * W;
+  const int tid = threadIdx.x;
+  const int g = tid % G;
+  const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
+  const bool active = i < re;
+  double xi[D], acc[D], fprev[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xi[k] = active ? X[(size_t)i * D + k] : 0.0;
+    fprev[k] = (active && g == 0) ? Fprev[(size_t)(i - rb) * D + k] : 0.0;
+    acc[k] = 0.0;
+  }
+  const double di = active ? dp1[i] : 1.0;
+  const bool row_ok = !active || (vertex_ok<D>(xi, di) && (REPEL_ONE || weight_ok(c.repel)));
+  const int e0 = active ? ip[i] : 0;
+  const int e1 = active ? ip[i + 1] : 0;
+  for (int t0 = 0; t0 < n; t0 += kStreamTile) {  // :151-167, j ascending
+    const int cnt = min(kStreamTile, n - t0);
+    __syncthreads();  // the previous tile has been consumed
+    bool ok = row_ok;
+    for (int q = tid; q < cnt; q += kGrpT) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        const double v = X[(size_t)(t0 + q) * D + k];
+        rec[q * W + k] = v;
+        ok = ok && coord_ok(v);
+      }
+      const double w = dp1[t0 + q];
+      rec[q * W + D] = w;
+      ok = ok && weight_ok(w);
+    }
+    if (__syncthreads_and(ok) && G > 1) {  // block-uniform: row and tile in the domain
+      pipelined_group_sum<D, G, kGrpT>(cnt, tid, g, tb, [&](int q, double (&t)[D]) {
+        const int jj = min(q, cnt - 1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+        rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
+        if (q >= cnt)
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[k] = 0.0;
+      }, acc);
+    } else {
+      const bool rok = active && vertex_ok<D>(xi, di) && (REPEL_ONE || weight_ok(c.repel));
+      for (int j0 = 0; j0 < cnt; j0 += G) {
+        double t[1][D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[0][k] = 0.0;
+        const int j = j0 + g;
+        if (active && j < cnt) {
+          const double* xj = &rec[j * W];
+          if (rok && vertex_ok<D>(xj, rec[j * W + D]))
+            rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+          else
+            rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+        }
+        group_add<D, G, 1>(t, tid, g, min(G, cnt - j0), active && g == 0, tb, acc);
+      }
+      if (G > 1)  // group_add leaves the sum in the group's first lane only
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = __shfl(acc[k], (tid - g) & 63);
+    }
+  }
+  // :169-203, CSR order; neighbours from X (per-edge domain test)
+  const bool xi_ok = all_coord_ok<D>(xi);
+  if (G > 1) {
+    pipelined_group_sum<D, G, kGrpT>(e1 - e0, tid, g, tb, [&](int q, double (&t)[D]) {
+      const int ee = min(e0 + q, e1 - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[k] = 0.0;
+      if (e1 > e0) {
+        const double* xj = X + (size_t)ix[ee] * D;
+        const double a = c.use_weights ? dx[ee] : 1.0;
+        if (xi_ok && all_coord_ok<D>(xj))
+          attr_edge<D, true, LINEAR>(xi, xj, a, di, c, t);
+        else
+          attr_edge<D, false>(xi, xj, a, di, c, t);
+      }
+      if (e0 + q >= e1)
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = 0.0;
+    }, acc);
+  } else {
+    for (int e = e0; e < e1; ++e) {
+      const double* xj = X + (size_t)ix[e] * D;
+      const double a = c.use_weights ? dx[e] : 1.0;
+      if (xi_ok && all_coord_ok<D>(xj))
+        attr_edge<D, true>(xi, xj, a, di, c, acc);
+      else
+        attr_edge<D, false>(xi, xj, a, di, c, acc);
+    }
+  }
+  if (active && g == 0)
+    finish_row<D>(i, i - rb, xi, acc, fprev, di, c, Fprev, Xnext, true);
+}
+
 // ---------------------------------------------------------------------------
 // host-side launch helpers
 
@@ -935,8 +1054,8 @@ int device_cus() {
 
 // Lanes per row of the small-level kernels.
 inline int grouped_lanes(int rows) {
-  int G = 1;  // lanes per row: aim for >= 64 K threads, at most one wave per row
-  while (G < 64 && (long long)rows * G < 65536) G *= 2;
+  int G = 1;  // lanes per row: aim for >= 128 K lanes, at most one wave per row
+  while (G < 64 && (long long)rows * G < 131072) G *= 2;  // n = 4373: G = 32 (175 us, G = 16: 211)
   if (const char* e = std::getenv("GE_GRP_G")) {  // tuning / test override
     const int g = std::atoi(e);
     if (g >= 1 && g <= 64 && (g & (g - 1)) == 0) G = g;
@@ -1022,25 +1141,31 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
   }
 }
 
-// Small levels (n <= grouped_cap): fa_grouped_step, one launch per iteration.
+// Small levels (n <= grouped_cap: fa_grouped_step) and mid-size ones (n <=
+// stream_max: fa_grouped_stream): one launch per iteration.
 template <int D>
 void launch_grouped_step(hipStream_t s, int n, int rb, int re, const int* ip, const int* ix,
                          const double* dx, const double* X, const double* dp1, const FaConst& c,
                          double* Fprev, double* Xnext) {
   const int rows = re - rb;
   if (rows <= 0) return;
-  const size_t lds = grouped_lds_bytes(n, D);
+  const bool stream = n > grouped_cap(D);
+  const size_t lds = stream ? stream_lds_bytes(D) : grouped_lds_bytes(n, D);
   auto go = [&](auto GG) {
     constexpr int GC = decltype(GG)::value;
     const int nb = (rows + kGrpT / GC - 1) / (kGrpT / GC);
     auto one = [&](auto RO, auto LI) {
       constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
+      const void* fn = stream ? reinterpret_cast<const void*>(&fa_grouped_stream<D, GC, R1, LIN>)
+                              : reinterpret_cast<const void*>(&fa_grouped_step<D, GC, R1, LIN>);
       if (lds > 65536)  // above the default dynamic-LDS limit
-        GE_HIP(hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&fa_grouped_step<D, GC, R1, LIN>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL((fa_grouped_step<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s, n, rb,
-                         re, ip, ix, dx, X, dp1, c, Fprev, Xnext);
+        GE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      if (stream)
+        hipLaunchKernelGGL((fa_grouped_stream<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s, n,
+                           rb, re, ip, ix, dx, X, dp1, c, Fprev, Xnext);
+      else
+        hipLaunchKernelGGL((fa_grouped_step<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s, n,
+                           rb, re, ip, ix, dx, X, dp1, c, Fprev, Xnext);
     };
     const bool lin = !c.linlog && c.delta == 1.0;
     using T = std::true_type;
@@ -1149,7 +1274,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   }
   dispatch_dim(pl->dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    if (pl->p.mode == GE_MODE_STRICT && pl->n <= grouped_cap(D) && !std::getenv("GE_GRP_SPLIT")) {
+    if (pl->p.mode == GE_MODE_STRICT && pl->n <= stream_max() && !std::getenv("GE_GRP_SPLIT")) {
       launch_grouped_step<D>(s, pl->n, pl->rb, pl->re, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p,
                              pl->c, pl->fprev.p, xn);
       if (ev) GE_HIP(hipEventRecord(ev[1], s));

@@ -70,6 +70,7 @@ def test_fa_degree_classes(ctx, oracle, monkeypatch, use_weights, tiles):
     """Rows of every degree class of the attraction kernel (ge_rows.hpp): light,
     wave-per-row (> 32 edges) and block-per-row (> 2048 edges, several chunks);
     with GE_ROWS_TILES=1 the tiles (<= 1024 entries) and block-per-row beyond."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
     monkeypatch.setenv("GE_ROWS_TILES", tiles)
     A = G.with_hubs(G.rmat(6000, 30000, seed=11), [(5, 4500), (17, 2100), (900, 300)])
     A = (A[0], A[1], np.random.RandomState(2).uniform(0.5, 2.0, len(A[1])))
@@ -87,6 +88,7 @@ def test_fa_row_tiles(ctx, oracle, monkeypatch, dim, segments):
     """Tiled CSR rows: rows at and around the tile capacity (tile vs heavy),
     tiles closed by the row limit and by the entry limit, isolated rows, every
     dimension; heavy rows as binade-sum segments or whole rows (GE_ROWS_SEGMENTS)."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
     monkeypatch.setenv("GE_ROWS_TILES", "1")
     monkeypatch.setenv("GE_ROWS_SEGMENTS", segments)
     A = G.with_degrees(G.rmat(5000, 20000, seed=dim), {7: 1023, 8: 1024, 9: 1025, 300: 700,
@@ -105,6 +107,7 @@ def test_fa_heavy_segments_binade_and_fallback(ctx, oracle, monkeypatch, scale):
     for the binade (|t/ulp| >= 2^36) and 1e-300 pushes the weighted degrees (and
     so the repulsion sums) towards the subnormal range: both fall back to the
     serial in-order sum.  Bit-exact either way."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
     monkeypatch.setenv("GE_ROWS_TILES", "1")
     A = G.with_degrees(G.rmat(7000, 28000, seed=4), {3: 5000, 11: 2600, 12: 513}, seed=5)
     A = (A[0], A[1], A[2] * scale)
@@ -118,6 +121,7 @@ def test_fa_heavy_segments_binade_and_fallback(ctx, oracle, monkeypatch, scale):
 def test_fa_row_tiles_graph_replay(ctx, oracle, monkeypatch):
     """Tiles + heavy rows on the side stream inside a captured graph (>= 128
     iterations replay 32-iteration graphs with the fork/join events)."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
     monkeypatch.setenv("GE_ROWS_TILES", "1")
     A = G.with_degrees(G.rmat(3300, 12000, seed=21), {5: 1500, 6: 900}, seed=2)
     X0 = G.random_coords(3300, 2, seed=6)
@@ -129,6 +133,7 @@ def test_fa_row_tiles_graph_replay(ctx, oracle, monkeypatch):
 def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
     """fa_repulse_strict with R row slots x 8/R partners in flight per lane
     (row shards of N GPUs pick small R), ragged tiles and slot counts."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
     monkeypatch.setenv("GE_REP_R", R)
     A = G.rmat(9000, 60000, seed=3)
     n = len(A[0]) - 1
@@ -178,6 +183,22 @@ def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim, split):
     X0 = G.random_coords(n, dim, seed=int(grp))
     want = oracle.force_atlas(A, dim, coords=X0, iterations=4)
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=4), want)
+
+
+@pytest.mark.parametrize("grp", ["0", "4", "16", "64"])
+@pytest.mark.parametrize("n,dim", [(4500, 3), (7000, 2), (3500, 4)])
+def test_fa_grouped_stream(ctx, oracle, monkeypatch, grp, n, dim):
+    """Mid-size levels (fa_grouped_stream): records streamed through LDS in tiles
+    of 2048, G lanes per row (0 = default choice), neighbours read from X; a
+    coordinate outside the exact-division domain sends one tile (and the rows
+    next to it) through the general bodies."""
+    if grp != "0":
+        monkeypatch.setenv("GE_GRP_G", grp)
+    A = G.with_degrees(G.rmat(n, 5 * n, seed=n), {17: 700}, seed=1)
+    X0 = G.random_coords(n, dim, seed=int(grp) + 1)
+    X0[2500, 0] = 1e-70
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=3)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=3), want)
 
 
 def test_fa_small_level_graph_replay(ctx, oracle):
