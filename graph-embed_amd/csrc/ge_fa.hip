@@ -1290,6 +1290,33 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   if (ev) GE_HIP(hipEventRecord(ev[2], s));
 }
 
+// ge_fa_plan_attract: the row kernels alone on a caller-supplied repulsion sum
+// (profiling: the repulsion interval is empty).
+static void plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, double* xn) {
+  hipStream_t s = pl->ctx->stream;
+  hipEvent_t* ev = nullptr;
+  if (pl->profiling) {
+    if (pl->next_event + 3 > pl->events.size()) {
+      for (int k = 0; k < 3 * 64; ++k) {
+        hipEvent_t e;
+        GE_HIP(hipEventCreate(&e));
+        pl->events.push_back(e);
+      }
+    }
+    ev = &pl->events[pl->next_event];
+    pl->next_event += 3;
+    GE_HIP(hipEventRecord(ev[0], s));
+    GE_HIP(hipEventRecord(ev[1], s));
+  }
+  dispatch_dim(pl->dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    launch_attract<D>(s, pl->rc, pl->rstreams, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, frep,
+                      pl->fprev.p, xn, pl->c);
+  });
+  GE_HIP(hipGetLastError());
+  if (ev) GE_HIP(hipEventRecord(ev[2], s));
+}
+
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
                    const double* d_dx, int dim, double* d_x, int iterations,
                    const ge_fa_params& p) {
@@ -1403,6 +1430,14 @@ int ge_fa_plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
     GE_REQUIRE(pl && xc && xn && xc != xn, "bad plan step arguments");
     ge::DeviceGuard g(pl->ctx);
     ge::plan_step(pl, xc, xn);
+  });
+}
+
+int ge_fa_plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, double* xn) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && xc && xn && frep && xc != xn, "bad plan attract arguments");
+    ge::DeviceGuard g(pl->ctx);
+    ge::plan_attract(pl, xc, frep, xn);
   });
 }
 

@@ -62,6 +62,7 @@ _SIGS = {
                                          ctypes.c_int, ctypes.POINTER(FaParams), ctypes.c_int,
                                          ctypes.c_int, ctypes.POINTER(_vp)]),
     "ge_fa_plan_step": (ctypes.c_int, [_vp, _vp, _vp]),
+    "ge_fa_plan_attract": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "ge_fa_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ge_fa_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double), _ip]),
@@ -339,6 +340,11 @@ class FaPlan:
 
     def step(self, d_x_cur, d_x_next):
         _check(lib().ge_fa_plan_step(self.h, _vp(d_x_cur), _vp(d_x_next)))
+
+    def attract(self, d_x_cur, d_frep, d_x_next):
+        """Attraction + gravity + update alone on supplied repulsion sums
+        (ge_fa_plan_attract)."""
+        _check(lib().ge_fa_plan_attract(self.h, _vp(d_x_cur), _vp(d_frep), _vp(d_x_next)))
 
     def set_profiling(self, on):
         _check(lib().ge_fa_plan_set_profiling(self.h, int(on)))

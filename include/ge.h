@@ -79,6 +79,14 @@ int ge_fa_plan_create(ge_ctx* ctx, int n, int nnz, const int* d_indptr,
 /* d_x_cur: all n*dim coordinates of this iteration; writes rows
  * [row_begin,row_end) of d_x_next (must not alias d_x_cur). */
 int ge_fa_plan_step(ge_fa_plan* plan, const double* d_x_cur, double* d_x_next);
+/* The second half of the iteration alone -- attraction in CSR order, gravity,
+ * swing and update (include/forceatlas.hpp:169-269) -- with the repulsion sums
+ * supplied by the caller (d_frep: (row_end - row_begin)*dim, the value each
+ * row's force holds after :151-167).  For measuring the attraction pass at
+ * sizes whose all-pairs repulsion is out of reach (configs[4]).  Always runs
+ * the CSR row kernels (tiles / heavy segments), also for small levels. */
+int ge_fa_plan_attract(ge_fa_plan* plan, const double* d_x_cur, const double* d_frep,
+                       double* d_x_next);
 /* Kernel timing with HIP events on the plan's stream (0 = off). */
 int ge_fa_plan_set_profiling(ge_fa_plan* plan, int enable);
 /* Average device ms per launch of the repulsion and attraction/update kernels

@@ -1,0 +1,88 @@
+"""configs[4] (C5): the attraction pass on a 100M-vertex / 800M-draw R-MAT --
+rocprof HBM-roofline report on the attraction SpMV.
+
+All-pairs repulsion at n = 1e8 (1e16 pairs per iteration) is out of reach, so
+this times the second half of the iteration alone (ge_fa_plan_attract: CSR
+attraction in stored order + gravity + swing + update, bit-exact machinery of
+the full path) on a SYNTHETIC repulsion sum: Frep[i][k] = (deg_i + 1) * 1e6 *
+U(-1, 1), the scale of a repulsion over ~1e8 vertices.  Coordinates U(-1, 1)
+(torch generator, seed 1).  Prints one JSON line; kernel times are HIP events
+on the plan's stream (tile + heavy-segment + heavy-finish kernels, fork to join).
+
+Algorithmic bytes per pass: 12*nnz + 52*n + 4 (int32 indptr /
+indices, fp64 weights, read x, write x_next; fp64 d = 3).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "graph-embed_amd", "py"))
+import ge_amd as ge  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000_000)
+    ap.add_argument("--draws", type=int, default=800_000_000)
+    ap.add_argument("--seed", type=int, default=12345)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    a = ap.parse_args()
+    dim = 3
+    t0 = time.perf_counter()
+    A = ge.rmat_csr(a.n, a.draws, seed=a.seed)
+    n, nnz = len(A[0]) - 1, int(A[0][-1])
+    print(f"R-MAT n={n} nnz={nnz} max deg={int(np.diff(A[0]).max())} "
+          f"generated in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    dev = torch.device("cuda:0")
+    ip = torch.from_numpy(A[0]).to(dev)
+    ix = torch.from_numpy(A[1]).to(dev)
+    dx = torch.from_numpy(A[2]).to(dev)
+    deg = torch.diff(ip).to(torch.float64)
+    del A
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    x = torch.rand(n, dim, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+    frep = (torch.rand(n, dim, dtype=torch.float64, device=dev, generator=g) * 2 - 1) * \
+        ((deg + 1) * 1e6)[:, None]
+    y = torch.empty_like(x)
+    ctx = ge.Context(0)
+    t0 = time.perf_counter()
+    plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), dim, 0, n)
+    print(f"plan {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    for _ in range(a.warmup):
+        plan.attract(x.data_ptr(), frep.data_ptr(), y.data_ptr())
+    ctx.sync()
+    plan.set_profiling(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        plan.attract(x.data_ptr(), frep.data_ptr(), y.data_ptr())
+    ctx.sync()
+    wall = (time.perf_counter() - t0) / a.steps
+    _, att_ms, launches = plan.kernel_ms()
+    finite = bool(torch.isfinite(y).all().item())
+    plan.close()
+    ctx.close()
+    bytes_alg = 12 * nnz + 52 * n + 4
+    gbs = bytes_alg / (att_ms * 1e-3) / 1e9
+    print(json.dumps({
+        "workload": "C5 (BASELINE.json configs[4]) attraction pass: Graph500 R-MAT "
+                    f"{a.n} ids, {a.draws} draws, d = 3, strict fp64, synthetic repulsion sums",
+        "n": n, "nnz": nnz, "passes_per_s": 1e3 / att_ms, "edges_per_s": nnz * 1e3 / att_ms,
+        "avg_pass_ms": att_ms, "wall_ms_per_pass": wall * 1e3, "launches": launches,
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_pass": bytes_alg},
+        "finite": finite}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -277,6 +277,34 @@ def test_fa_plan_row_shards_compose(ctx, oracle):
     assert np.array_equal(x.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("tiles", ["1", "0"])
+def test_fa_plan_attract_on_supplied_repulsion(ctx, oracle, monkeypatch, tiles):
+    """ge_fa_plan_attract: the attraction/update half of the iteration on a
+    caller-supplied repulsion sum (the oracle's force rows with attract = 0 and
+    gravity = 0, i.e. exactly the repulsion) equals one full oracle iteration;
+    heavy rows as binade segments (tiles) or classed rows."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("GE_ROWS_TILES", tiles)
+    A = G.with_degrees(G.rmat(5000, 20000, seed=31), {2: 3000, 9: 700}, seed=3)
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=12)
+    deg = oracle.degrees(A)
+    frep = oracle.fa_forces_rows(A, X0, deg, 0, n, attract=0.0, gravity=0.0)
+    dev = torch.device("cuda:0")
+    ip = torch.from_numpy(A[0].astype(np.int32)).to(dev)
+    ix = torch.from_numpy(A[1].astype(np.int32)).to(dev)
+    dx = torch.from_numpy(A[2]).to(dev)
+    x = torch.from_numpy(X0.copy()).to(dev)
+    f = torch.from_numpy(frep).to(dev)
+    y = torch.empty_like(x)
+    plan = ctx.fa_plan(n, len(A[1]), ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), 3, 0, n)
+    plan.attract(x.data_ptr(), f.data_ptr(), y.data_ptr())
+    ctx.sync()
+    plan.close()
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=1)
+    assert np.array_equal(y.cpu().numpy(), want)
+
+
 # --------------------------------------------------------------------------
 # multilevel
 
