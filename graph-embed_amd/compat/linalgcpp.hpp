@@ -1,11 +1,13 @@
-// compat/linalgcpp.hpp -- see compat/sparsematrix.hpp.  Also the Timer the
-// reference's drivers use (examples/embedder.cpp:219-222).
+// compat/linalgcpp.hpp -- see compat/sparsematrix.hpp and compat/parser.hpp
+// (graph readers).  Also the Timer the reference's drivers use
+// (examples/embedder.cpp:219-222).
 #ifndef GE_COMPAT_LINALGCPP_HPP
 #define GE_COMPAT_LINALGCPP_HPP
 
 #include <chrono>
 #include <vector>
 
+#include "parser.hpp"
 #include "sparsematrix.hpp"
 
 namespace linalgcpp {
