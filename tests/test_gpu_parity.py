@@ -252,11 +252,18 @@ def test_fa_fast_mode_tolerance(ctx, oracle):
     assert rel_err(fast, strict) < REL_TOL_FAST
 
 
-def test_fa_plan_row_shards_compose(ctx, oracle):
+@pytest.mark.parametrize("path", ["fused", "rows"])
+def test_fa_plan_row_shards_compose(ctx, oracle, monkeypatch, path):
     """Two row shards stepping over a shared coordinate array (what each rank of
-    the multi-GPU path runs between all-gathers) equal the unsharded iteration."""
+    the multi-GPU path runs between all-gathers) equal the unsharded iteration:
+    small-level fused kernel, or the large-level kernels (repulsion row slots,
+    row tiles, heavy-row segments inside a shard)."""
     torch = pytest.importorskip("torch")
-    A = G.largest_component(G.rmat(2600, 20000, seed=21))
+    if path == "rows":
+        monkeypatch.setenv("GE_STREAM_MAX", "0")
+        monkeypatch.setenv("GE_ROWS_TILES", "1")
+    A = G.largest_component(G.with_degrees(G.rmat(2600, 20000, seed=21), {4: 1300, 1700: 600},
+                                           seed=2))
     n = len(A[0]) - 1
     X0 = G.random_coords(n, 3, seed=8)
     dev = torch.device("cuda:0")
