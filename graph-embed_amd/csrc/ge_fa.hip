@@ -474,7 +474,9 @@ __device__ __forceinline__ void pipelined_group_sum(int nitems, int tid, int g, 
     const int cur = (c0 / G) & 1;
     wave_lds_sync();
     const bool more = c0 + G < nitems;
-    if (more) term(c0 + G + g, t);  // next chunk, independent of the adds below
+    // next chunk, independent of the adds below; evaluated unconditionally (the
+    // terms clamp their item) so the compiler can interleave it with the chain
+    term(c0 + G + g, t);
     const double* reg = tb + cur * T * D + base * D;
     const int cnt = min(G, nitems - c0);
     if constexpr (kLaneDim) {
@@ -746,6 +748,42 @@ void launch_small(hipStream_t s, int n, int nnz, const int* ip, const int* ix, c
 // terms in j order (pipelined_group_sum).  Every block stages all n records in
 // LDS; the exact-division domain is checked once per block.
 
+// Records [first, first + cnt) of X / dp1 into rec (Rec<D>::W doubles each) by
+// the T threads of the block: SU records per thread per round with all their
+// loads issued before the stores (a plain strided loop waits for one record at
+// a time).  Returns whether every staged value lies in the exact-division domain.
+template <int D, int T, int SU>
+__device__ __forceinline__ bool stage_records(const double* __restrict__ X,
+                                              const double* __restrict__ dp1, int first, int cnt,
+                                              double* rec) {
+  constexpr int W = Rec<D>::W;
+  bool ok = true;
+  for (int q0 = 0; q0 < cnt; q0 += T * SU) {
+    double v[SU][D + 1];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int q = min(q0 + (int)threadIdx.x + T * u, cnt - 1);  // clamped into the range
+#pragma unroll
+      for (int k = 0; k < D; ++k) v[u][k] = X[(size_t)(first + q) * D + k];
+      v[u][D] = dp1[first + q];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int q = q0 + (int)threadIdx.x + T * u;
+      if (q < cnt) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          rec[q * W + k] = v[u][k];
+          ok = ok && coord_ok(v[u][k]);
+        }
+        rec[q * W + D] = v[u][D];
+        ok = ok && weight_ok(v[u][D]);
+      }
+    }
+  }
+  return ok;
+}
+
 constexpr int kGrpT = 256;
 constexpr int grouped_cap(int D) { return (D + 1 <= 4) ? 3072 : 1536; }  // <= 96 KiB of records
 inline size_t grouped_lds_bytes(int n, int D) {
@@ -765,18 +803,8 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
   const int g = tid % G;
   const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
   const bool active = i < re;
-  bool ok = REPEL_ONE || weight_ok(repel);
-  for (int q = tid; q < n; q += kGrpT) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const double v = X[(size_t)q * D + k];
-      rec[q * W + k] = v;
-      ok = ok && coord_ok(v);
-    }
-    const double w = dp1[q];
-    rec[q * W + D] = w;
-    ok = ok && weight_ok(w);
-  }
+  const bool ok =
+      stage_records<D, kGrpT, 4>(X, dp1, 0, n, rec) && (REPEL_ONE || weight_ok(repel));
   __syncthreads();
   double xi[D], acc[D];
 #pragma unroll
@@ -841,23 +869,17 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
   const int g = tid % G;
   const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
   const bool active = i < re;
-  bool ok = REPEL_ONE || weight_ok(c.repel);
-  for (int q = tid; q < n; q += kGrpT) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const double v = X[(size_t)q * D + k];
-      rec[q * W + k] = v;
-      ok = ok && coord_ok(v);
-    }
-    const double w = dp1[q];
-    rec[q * W + D] = w;
-    ok = ok && weight_ok(w);
-  }
+  const bool ok =
+      stage_records<D, kGrpT, 4>(X, dp1, 0, n, rec) && (REPEL_ONE || weight_ok(c.repel));
   double xi[D], acc[D], fprev[D];
   const int e0 = active ? ip[i] : 0;
   const int e1 = active ? ip[i + 1] : 0;
 #pragma unroll
   for (int k = 0; k < D; ++k) fprev[k] = (active && g == 0) ? Fprev[(size_t)(i - rb) * D + k] : 0.0;
+  // the CSR row's first chunk, loaded while the records are being staged
+  const int pe = min(e0 + g, e1 - 1);
+  const int pix = e1 > e0 ? ix[pe] : 0;
+  const double pdx = (e1 > e0 && c.use_weights) ? dx[pe] : 1.0;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < D; ++k) {
@@ -879,7 +901,9 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
       const int ee = min(e0 + q, e1 - 1);
 #pragma unroll
       for (int k = 0; k < D; ++k) t[k] = 0.0;
-      attr_edge<D, true, LINEAR>(xi, &rec[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, di, c, t);
+      const int j = q < G ? pix : ix[ee];  // chunk 0 (q = g) was prefetched
+      const double a = q < G ? pdx : (c.use_weights ? dx[ee] : 1.0);
+      attr_edge<D, true, LINEAR>(xi, &rec[j * W], a, di, c, t);
       if (e0 + q >= e1)
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
@@ -964,18 +988,7 @@ fa_grouped_stream(int n, int rb, int re, const int* __restrict__ ip, const int* 
   for (int t0 = 0; t0 < n; t0 += kStreamTile) {  // :151-167, j ascending
     const int cnt = min(kStreamTile, n - t0);
     __syncthreads();  // the previous tile has been consumed
-    bool ok = row_ok;
-    for (int q = tid; q < cnt; q += kGrpT) {
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        const double v = X[(size_t)(t0 + q) * D + k];
-        rec[q * W + k] = v;
-        ok = ok && coord_ok(v);
-      }
-      const double w = dp1[t0 + q];
-      rec[q * W + D] = w;
-      ok = ok && weight_ok(w);
-    }
+    const bool ok = stage_records<D, kGrpT, 8>(X, dp1, t0, cnt, rec) && row_ok;
     if (__syncthreads_and(ok) && G > 1) {  // block-uniform: row and tile in the domain
       pipelined_group_sum<D, G, kGrpT>(cnt, tid, g, tb, [&](int q, double (&t)[D]) {
         const int jj = min(q, cnt - 1);
