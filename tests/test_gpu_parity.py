@@ -171,7 +171,7 @@ def test_fa_small_kernel_out_of_domain_start(ctx, oracle, monkeypatch, small_max
 
 
 @pytest.mark.parametrize("split", ["0", "1"])
-@pytest.mark.parametrize("grp", ["1", "2", "4", "16", "64"])
+@pytest.mark.parametrize("grp", ["1", "2", "4", "16", "32", "64"])
 @pytest.mark.parametrize("n,dim", [(700, 3), (1400, 4), (2900, 2)])
 def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim, split):
     """Small levels: G lanes per row, in-order group sums; one fused launch per
@@ -185,7 +185,7 @@ def test_fa_grouped_repulsion(ctx, oracle, monkeypatch, grp, n, dim, split):
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=4), want)
 
 
-@pytest.mark.parametrize("grp", ["0", "4", "16", "64"])
+@pytest.mark.parametrize("grp", ["0", "4", "16", "32", "64"])
 @pytest.mark.parametrize("n,dim", [(4500, 3), (7000, 2), (3500, 4)])
 def test_fa_grouped_stream(ctx, oracle, monkeypatch, grp, n, dim):
     """Mid-size levels (fa_grouped_stream): records streamed through LDS in tiles
