@@ -1257,7 +1257,7 @@ static void plan_init(ge_fa_plan* pl) {
     }
     // single level: a row's sum starts at its repulsion over all n vertices, far
     // above the edge terms, so heavy rows split into binade-sum segments
-    classify_rows(ids, deg, order, pl->rc, true);
+    classify_rows(ids, deg, order, pl->rc, kSegBinade);
     pl->rows.alloc(order.size());
     pl->rows.upload(order.data(), order.size(), s);
     pl->rc.bind(pl->rows.p);

@@ -760,13 +760,14 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       deg[q] = h_ip[v + 1] - h_ip[v];
     }
     // the in-aggregate repulsion is not far above the external pulls (measured
-    // at C3: every heavy row left the binade), so heavy rows stay whole
-    classify_rows(rows, deg, erows, pl->ecls, false);
+    // at C3: every heavy row left the binade), so heavy rows store their terms
+    std::vector<int> hdeg;
+    classify_rows(rows, deg, erows, pl->ecls, kSegStore, &hdeg);
     pl->ecode.alloc(std::max(h_ip[pl->n], 1));
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
     pl->ecls.bind(pl->erows.p);
-    pl->rstreams.attach(pl->ecls, pl->dim, st);
+    pl->rstreams.attach(pl->ecls, pl->dim, st, hdeg);
   }
   struct Item { int a, r0; double work; };
   std::vector<Item> its;

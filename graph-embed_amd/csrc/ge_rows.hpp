@@ -60,6 +60,9 @@ struct RowClasses {
   long long* hacc = nullptr;      // nheavy x D x {S, A}: binade sums of the segments (zeroed)
   int* hflag = nullptr;           // nheavy: a segment could not use the binade sum
   int* nfall = nullptr;           // count of heavy-row passes summed serially (GE_ROWS_STATS)
+  double* hterm = nullptr;        // kSegStore: the heavy rows' terms, row h at hoff[h], dim-major
+  const long long* hoff = nullptr;
+  int seg_mode = 0;               // kSegBinade / kSegStore when nseg > 0
   int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0, nseg = 0;
   int tile_off = 0;  // where tile_ptr starts in the host array
   int seg_off = 0;   // where seg starts in the host array
@@ -74,10 +77,17 @@ struct RowClasses {
 // Host: order `ids` (row ids with their degrees) into classes; `out` gets the
 // row list followed by the tile boundaries (upload all of it, then bind()).
 // GE_ROWS_MED / GE_ROWS_HEAVY / GE_ROWS_TILES override the choices (tuning).
-// segments: heavy rows may be split into binade-sum segments (the policy's
-// row sums start far above its edge terms: single-level forceAtlas).
+// Heavy rows in tile mode are split into segments of <= kTileCap entries,
+// evaluated as tiles, and then summed by one of:
+//   kSegBinade  integer sums in the binade of the row's force (its sum starts far
+//               above its edge terms: single-level forceAtlas), serial fallback;
+//   kSegStore   the terms stored in HBM, then one wave per row adds them in order
+//               (the multilevel member rows, whose sums leave the binade).
+// kSegNone keeps heavy rows whole (one block per row, on a side stream).
+constexpr int kSegNone = 0, kSegBinade = 1, kSegStore = 2;
 inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& deg,
-                          std::vector<int>& out, RowClasses& rc, bool segments) {
+                          std::vector<int>& out, RowClasses& rc, int seg_mode,
+                          std::vector<int>* heavy_deg = nullptr) {
   bool tiles = ids.size() >= (size_t)kTileMinRows;
   if (const char* e = std::getenv("GE_ROWS_TILES")) tiles = std::atoi(e) != 0;
   // few rows (a small level): latency, not throughput -- rows of more than 4
@@ -86,8 +96,12 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
   if (const char* e = std::getenv("GE_ROWS_MED")) med = std::atoi(e);
   if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::min(std::atoi(e), tiles ? kTileCap : 1 << 30);
   out.clear();
+  if (heavy_deg) heavy_deg->clear();
   for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] > heavy) out.push_back(ids[q]);
+    if (deg[q] > heavy) {
+      out.push_back(ids[q]);
+      if (heavy_deg) heavy_deg->push_back(deg[q]);
+    }
   rc.nheavy = (int)out.size();
   std::vector<int> tp;
   if (tiles) {
@@ -118,8 +132,9 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
   out.insert(out.end(), tp.begin(), tp.end());
   // heavy rows as segments of <= kTileCap entries (tile mode; GE_ROWS_SEGMENTS=0: whole rows
   // on a side stream instead)
-  bool segs = tiles && segments;
+  bool segs = tiles && seg_mode != kSegNone;
   if (const char* e = std::getenv("GE_ROWS_SEGMENTS")) segs = segs && std::atoi(e) != 0;
+  rc.seg_mode = segs ? seg_mode : kSegNone;
   rc.seg_off = (int)out.size();
   rc.nseg = 0;
   if (segs) {
@@ -527,6 +542,82 @@ __global__ void __launch_bounds__(kRowT) heavy_finish_kernel(RowClasses L, P p) 
   if (lane == 0) L.hflag[h] = 0;
 }
 
+// kSegStore, phase A: the terms of one segment of a heavy row, stored
+// dimension-major in the row's region of L.hterm.
+template <int D, class P>
+__device__ __forceinline__ void segment_store(const RowClasses& L, const P& p, int q) {
+  using State = typename P::State;
+  const int tid = threadIdx.x;
+  const int h = L.seg[3 * q], a = L.seg[3 * q + 1], b = L.seg[3 * q + 2];
+  State st;
+  p.load(L.rows[h], st);
+  const int deg = st.e1 - st.e0;
+  double* out = L.hterm + L.hoff[h];
+  constexpr int U = kTileCap / kRowT;
+  double tt[U][D];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = st.e0 + min(a + tid + kRowT * u, b - 1);
+#pragma unroll
+    for (int k = 0; k < D; ++k) tt[u][k] = 0.0;
+    p.term(st, e, tt[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int l = a + tid + kRowT * u;
+    if (l < b)
+#pragma unroll
+      for (int k = 0; k < D; ++k) out[(size_t)k * deg + l] = tt[u][k];
+  }
+}
+
+// kSegStore, phase B: one wave per heavy row adds the stored terms in order
+// (lane k: dimension k) while the whole wave streams the next chunk of them
+// from HBM into LDS; then gravity and the update.
+constexpr int kStoreChunk = 512;  // terms per dimension per chunk
+template <int D, class P>
+__global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p) {
+  __shared__ __attribute__((aligned(16))) double buf[2][D * kStoreChunk];
+  const int lane = threadIdx.x;
+  const int h = blockIdx.x;
+  typename P::State st;
+  p.load(L.rows[h], st);
+  const int deg = st.e1 - st.e0;
+  const double* in = L.hterm + L.hoff[h];
+  const int kd = lane < D ? lane : D - 1;
+  double a = lane_dim_value<D>(st.acc, kd);
+  constexpr int PER = D * kStoreChunk / 64;  // values per lane per chunk
+  double v[PER];
+  auto fetch = [&](int c0) {  // chunk [c0, c0 + kStoreChunk) of every dimension
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const int x = lane + 64 * r;  // dimension x / kStoreChunk, item x % kStoreChunk
+      const int k = x / kStoreChunk, l = c0 + x % kStoreChunk;
+      v[r] = l < deg ? in[(size_t)k * deg + l] : 0.0;
+    }
+  };
+  auto put = [&](double* dst) {
+#pragma unroll
+    for (int r = 0; r < PER; ++r) dst[lane + 64 * r] = v[r];
+  };
+  if (deg > 0) {
+    fetch(0);
+    put(buf[0]);
+  }
+  int c = 0;
+  for (int c0 = 0; c0 < deg; c0 += kStoreChunk, ++c) {
+    wave_lds_sync();  // chunk c is in buf[c & 1]
+    const bool more = c0 + kStoreChunk < deg;
+    if (more) fetch(c0 + kStoreChunk);  // in flight during the adds below
+    a = lane_chain(a, buf[c & 1] + kd * kStoreChunk, min(kStoreChunk, deg - c0));
+    wave_lds_sync();
+    if (more) put(buf[(c + 1) & 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) st.acc[k] = __shfl(a, k);
+  p.finish(st, lane == 0);
+}
+
 // Tiles get their own kernel: without the heavy path's registers and LDS it
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
 template <int D, class P>
@@ -534,6 +625,8 @@ __global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
   if ((int)blockIdx.x < L.ntiles)
     tile_rows<D>(L, p, blockIdx.x, lds);
+  else if (L.seg_mode == kSegStore)
+    segment_store<D>(L, p, blockIdx.x - L.ntiles);
   else
     segment_rows<D>(L, p, blockIdx.x - L.ntiles, lds);
 }
@@ -586,12 +679,25 @@ __global__ void __launch_bounds__(kRowT, GE_ROWS_MINBLOCKS) classed_rows_kernel(
 // Per-plan row resources: the side stream + events for running whole heavy rows
 // beside the tiles, and the heavy rows' binade accumulators (segment mode).
 struct RowStreams {
-  DevBuf<long long> hacc;
+  DevBuf<long long> hacc, hoff;
   DevBuf<int> hflag, nfall;
+  DevBuf<double> hterm;
   int nheavy = 0;
-  // allocate and zero the accumulators of rc's heavy rows (segment mode)
-  void attach(RowClasses& rc, int D, hipStream_t s) {
+  // allocate (and zero) the heavy rows' segment buffers; deg: their entry
+  // counts in rows order (kSegStore)
+  void attach(RowClasses& rc, int D, hipStream_t s, const std::vector<int>& heavy_deg = {}) {
     if (rc.nseg == 0) return;
+    if (rc.seg_mode == kSegStore) {
+      std::vector<long long> off(rc.nheavy + 1, 0);
+      for (int h = 0; h < rc.nheavy; ++h) off[h + 1] = off[h] + (long long)heavy_deg.at(h) * D;
+      hoff.alloc(rc.nheavy + 1);
+      hoff.upload(off.data(), off.size(), s);
+      GE_HIP(hipStreamSynchronize(s));  // off is a local
+      hterm.alloc(std::max<long long>(off[rc.nheavy], 1));
+      rc.hoff = hoff.p;
+      rc.hterm = hterm.p;
+      return;
+    }
     hacc.alloc((size_t)rc.nheavy * 2 * D);
     hflag.alloc(rc.nheavy);
     GE_HIP(hipMemsetAsync(hacc.p, 0, sizeof(long long) * hacc.n, s));
@@ -636,10 +742,13 @@ struct RowStreams {
 template <int D, class P>
 inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
   const int tgrid = rc.ntiles + rc.nseg;
-  if (rc.nseg > 0) {  // heavy rows as segments, then their finish
+  if (rc.nseg > 0) {  // heavy rows as segments, then their sums and finish
     hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p);
-    hipLaunchKernelGGL((heavy_finish_kernel<D, P>), dim3((rc.nheavy + 3) / 4), dim3(kRowT), 0, s,
-                       rc, p);
+    if (rc.seg_mode == kSegStore)
+      hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy), dim3(64), 0, s, rc, p);
+    else
+      hipLaunchKernelGGL((heavy_finish_kernel<D, P>), dim3((rc.nheavy + 3) / 4), dim3(kRowT), 0,
+                         s, rc, p);
     return;
   }
   if (rc.ntiles > 0 && rc.nheavy > 0 && std::getenv("GE_ROWS_SERIAL")) {  // tuning: no overlap

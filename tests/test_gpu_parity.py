@@ -353,13 +353,17 @@ def test_faml_size_classes(ctx, oracle, sizes):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("R,U,tiles", [(1, 1, "0"), (1, 1, "1"), (1, 2, "1"), (1, 4, "0"),
-                                        (2, 1, "1"), (4, 1, "0")])
-def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles):
+@pytest.mark.parametrize("R,U,tiles,segs", [(1, 1, "0", "1"), (1, 1, "1", "1"), (1, 1, "1", "0"),
+                                             (1, 2, "1", "1"), (1, 4, "0", "1"), (2, 1, "1", "1"),
+                                             (4, 1, "0", "1")])
+def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs):
     """Streamed path (faml_big_repulse / faml_big_edges) with 1, 2 and 4 row
     slots per lane, ragged last items, and hub rows longer than one 64-edge chunk;
-    member rows tiled or classed (GE_ROWS_TILES)."""
+    member rows tiled or classed (GE_ROWS_TILES), heavy member rows as stored-term
+    segments + one chain wave per row, or whole rows on a side stream
+    (GE_ROWS_SEGMENTS=0)."""
     monkeypatch.setenv("GE_ROWS_TILES", tiles)
+    monkeypatch.setenv("GE_ROWS_SEGMENTS", segs)
     monkeypatch.setenv("GE_FAML_R", str(R))
     monkeypatch.setenv("GE_FAML_U", str(U))
     sizes = [3000, 700, 2203, 90, 1]
