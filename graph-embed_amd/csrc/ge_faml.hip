@@ -501,8 +501,14 @@ struct FamlRows {
   }
   __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
     const int code = ecode[e];
+    // the neighbour's (or its aggregate's) coordinates into registers before
+    // the branch, so a thread's gathers issue together
+    const double* src = code >= 0 ? Xc + (size_t)code * D : cA + (size_t)(-code - 1) * D;
+    double xv[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xv[k] = src[k];
     if (code >= 0) {  // internal entry (edge_code_kernel)
-      const double* xj = Xc + (size_t)code * D;
+      const double* xj = xv;
       const double wt = c.use_weights ? dx[e] : 1.0;
       if (s.row_ok && all_coord_ok<D>(xj))
         attr_edge<D, true>(s.xi, xj, wt, s.dip1, c, t);
@@ -510,7 +516,7 @@ struct FamlRows {
         attr_edge<D, false>(s.xi, xj, wt, s.dip1, c, t);
     } else {
       const double* ca = cA + (size_t)s.a * D;
-      const double* cb = cA + (size_t)(-code - 1) * D;
+      const double* cb = xv;
       if (s.row_ok && s.ca_ok && all_coord_ok<D>(cb))
         pull_edge<D, true>(ca, cb, s.mag, s.rmag, t);
       else
