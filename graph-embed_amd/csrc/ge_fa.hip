@@ -54,8 +54,19 @@ __global__ void degp1_kernel(int n, const int* __restrict__ ip, const double* __
   if (i >= n) return;
   double d;
   if (use_weights) {
+    // same serial adds; the loads of 16 entries are issued before their adds,
+    // so a hub row waits on one memory latency per 16 entries, not per entry
     d = 0.0;
-    for (int e = ip[i]; e < ip[i + 1]; ++e) d += dx[e];
+    const int e1 = ip[i + 1];
+    int e = ip[i];
+    for (; e + 16 <= e1; e += 16) {
+      double w[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) w[u] = dx[e + u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) d += w[u];
+    }
+    for (; e < e1; ++e) d += dx[e];
   } else {
     d = 1.0 * (ip[i + 1] - ip[i]);
   }
