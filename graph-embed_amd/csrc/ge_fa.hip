@@ -145,7 +145,40 @@ fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict
       // in the exact shared-reciprocal domain (ge_math.hpp)
       if (__syncthreads_and(ok)) {
         int jj = 0;
-        if (U > 1) {
+        if (nr == R) {
+          // every slot of the wave has rows: no per-slot branches, so the
+          // partner's LDS record is read once and the R rows' independent
+          // chains interleave
+          if constexpr (U == 1) {
+            for (; jj < cnt; ++jj) {
+              const double* xj = &tile[jj * W];
+              const double dj = tile[jj * W + D];
+#pragma unroll
+              for (int r = 0; r < R; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+            }
+          } else {
+            for (; jj + U <= cnt; jj += U) {
+              double t[U][R][D];
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const double* xj = &tile[(jj + u) * W];
+                const double dj = tile[(jj + u) * W + D];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                  for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
+                  rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
+                }
+              }
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                  for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
+            }
+          }
+        } else if (U > 1) {
           for (; jj + U <= cnt; jj += U) {
             double t[U][R][D];
 #pragma unroll
@@ -1142,7 +1175,9 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
     return;
   }
   // one block per CU, rows split evenly (rounded to whole 64-row wave slots)
-  const int blocks = std::max(1, std::min(cus, (rows + 63) / 64));
+  int cap = cus;
+  if (const char* e = std::getenv("GE_REP_BLOCKS")) cap = std::max(1, std::atoi(e));  // tests
+  const int blocks = std::max(1, std::min(cap, (rows + 63) / 64));
   int per = (rows + blocks - 1) / blocks;
   per = (per + 63) / 64 * 64;
   const int nb = (rows + per - 1) / per;

@@ -142,6 +142,21 @@ def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
     assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3), want)
 
 
+@pytest.mark.parametrize("R", ["1", "2", "4", "8"])
+def test_fa_repulsion_full_row_slots(ctx, oracle, monkeypatch, R):
+    """Blocks that own thousands of rows, as at C2 (1M rows over 256 CUs): every
+    row slot of a wave is filled (the branch-free path with the partner's
+    record read once for all R rows), plus the ragged last chunk."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")
+    monkeypatch.setenv("GE_REP_R", R)
+    monkeypatch.setenv("GE_REP_BLOCKS", "2")  # 4544 rows per block
+    A = G.rmat(9000, 60000, seed=5)
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=9)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=3)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3), want)
+
+
 @pytest.mark.parametrize("hook", [("GE_SMALL_GENERAL_ONLY", "1"), ("GE_SMALL_HANDOVER", "37"),
                                   ("GE_SMALL_HANDOVER", "0")])
 def test_fa_small_kernel_handover(ctx, oracle, monkeypatch, hook):
