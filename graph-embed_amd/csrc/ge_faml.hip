@@ -336,7 +336,7 @@ faml_huge_init(int nrows, const int* __restrict__ rows, const int* __restrict__ 
 
 // R row slots per lane, U consecutive partners evaluated together (their terms
 // are then added in j order).
-template <int D, int R, int U>
+template <int D, int R, int U, bool REPEL_ONE>
 __global__ void __launch_bounds__(kHT)
 faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ Xp,
@@ -345,7 +345,7 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
   __shared__ __attribute__((aligned(16))) double tiles[kHT / 64][kBigW * WV];
   const int lane = threadIdx.x & 63;
   double* tile = tiles[threadIdx.x >> 6];
-  const bool repel_ok = weight_ok(repel);
+  const bool repel_ok = REPEL_ONE || weight_ok(repel);
   for (;;) {
     int q = 0;
     if (lane == 0) q = atomicAdd(queue, 1);
@@ -390,7 +390,38 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
       wave_lds_sync();
       if (__all(ok)) {
         int jj = 0;
-        if (U > 1) {
+        if (nr == R) {
+          // every row slot of the wave is used: no per-slot branches, so the
+          // partner record is read once for all R rows and the independent
+          // chains (R rows x U partners) interleave
+          if constexpr (U == 1) {
+            for (; jj < cnt; ++jj) {
+              const double* xj = &tile[jj * WV];
+              const double dj = tile[jj * WV + D];
+#pragma unroll
+              for (int r = 0; r < R; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+            }
+          } else {
+            for (; jj + U <= cnt; jj += U) {
+              double t[U][R][D];
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+#pragma unroll
+                  for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
+                  rep_pair<D, true, REPEL_ONE>(xi[r], &tile[(jj + u) * WV], di[r],
+                                               tile[(jj + u) * WV + D], repel, t[u][r]);
+                }
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                  for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
+            }
+          }
+        } else if (U > 1) {
           for (; jj + U <= cnt; jj += U) {
             double t[U][R][D];
 #pragma unroll
@@ -400,8 +431,8 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
 #pragma unroll
                 for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
                 if (r < nr)
-                  rep_pair<D, true, false>(xi[r], &tile[(jj + u) * WV], di[r],
-                                           tile[(jj + u) * WV + D], repel, t[u][r]);
+                  rep_pair<D, true, REPEL_ONE>(xi[r], &tile[(jj + u) * WV], di[r],
+                                               tile[(jj + u) * WV + D], repel, t[u][r]);
               }
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -416,7 +447,7 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
           const double dj = tile[jj * WV + D];
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (r < nr) rep_pair<D, true, false>(xi[r], xj, di[r], dj, repel, acc[r]);
+            if (r < nr) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
         }
       } else {
         for (int jj = 0; jj < cnt; ++jj) {
@@ -424,7 +455,7 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
           const double dj = tile[jj * WV + D];
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (r < nr) rep_pair<D, false, false>(xi[r], xj, di[r], dj, repel, acc[r]);
+            if (r < nr) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
         }
       }
     }
@@ -630,8 +661,12 @@ void launch_big_repulse(int code, int blocks, hipStream_t st, int nitems, const 
   switch (code) {
 #define GE_BIG_LAUNCH(RR, UU)                                                                 \
   case big_code(RR, UU):                                                                      \
-    hipLaunchKernelGGL((faml_big_repulse<D, RR, UU>), dim3(blocks), dim3(kHT), 0, st, nitems, \
-                       items, queue, pt_ip, X, DP, repel, F);                                 \
+    if (repel == 1.0)                                                                         \
+      hipLaunchKernelGGL((faml_big_repulse<D, RR, UU, true>), dim3(blocks), dim3(kHT), 0, st, \
+                         nitems, items, queue, pt_ip, X, DP, repel, F);                       \
+    else                                                                                      \
+      hipLaunchKernelGGL((faml_big_repulse<D, RR, UU, false>), dim3(blocks), dim3(kHT), 0,    \
+                         st, nitems, items, queue, pt_ip, X, DP, repel, F);                   \
     break;
     GE_BIG_VARIANTS(GE_BIG_LAUNCH)
 #undef GE_BIG_LAUNCH
@@ -648,10 +683,10 @@ int rep_occupancy(int dim, int code) {
     const void* k = nullptr;
     switch (code) {
 #define GE_BIG_KERNEL(RR, UU) \
-  case big_code(RR, UU): k = (const void*)faml_big_repulse<D, RR, UU>; break;
+  case big_code(RR, UU): k = (const void*)faml_big_repulse<D, RR, UU, false>; break;
       GE_BIG_VARIANTS(GE_BIG_KERNEL)
 #undef GE_BIG_KERNEL
-      default: k = (const void*)faml_big_repulse<D, 1, 1>;
+      default: k = (const void*)faml_big_repulse<D, 1, 1, false>;
     }
     GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kHT, 0));
   });

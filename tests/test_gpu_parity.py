@@ -368,12 +368,14 @@ def test_faml_size_classes(ctx, oracle, sizes):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("R,U,tiles,segs", [(1, 1, "0", "1"), (1, 1, "1", "1"), (1, 1, "1", "0"),
-                                             (1, 2, "1", "1"), (1, 4, "0", "1"), (2, 1, "1", "1"),
-                                             (4, 1, "0", "1")])
-def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs):
+@pytest.mark.parametrize("R,U,tiles,segs,repel", [
+    (1, 1, "0", "1", 1.0), (1, 1, "1", "1", 1.0), (1, 1, "1", "0", 1.0), (1, 2, "1", "1", 1.0),
+    (1, 4, "0", "1", 1.0), (2, 1, "1", "1", 1.0), (4, 1, "0", "1", 1.0), (1, 1, "1", "1", 1.5),
+    (2, 1, "1", "1", 0.75)])
+def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, repel):
     """Streamed path (faml_big_repulse / faml_big_edges) with 1, 2 and 4 row
-    slots per lane, ragged last items, and hub rows longer than one 64-edge chunk;
+    slots per lane (full and ragged items), repel = 1 and not, and hub rows longer
+    than one 64-edge chunk;
     member rows tiled or classed (GE_ROWS_TILES), heavy member rows as stored-term
     segments + one chain wave per row, or whole rows on a side stream
     (GE_ROWS_SEGMENTS=0)."""
@@ -390,8 +392,8 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs):
     m = len(sizes)
     cA = G.random_coords(m, 3, seed=m)
     rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17, repel=repel)
     assert np.array_equal(got, want)
 
 
