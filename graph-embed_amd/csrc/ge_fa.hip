@@ -94,6 +94,57 @@ struct Rec {
   static constexpr int W = (D + 1 <= 4) ? 4 : 8;  // doubles per LDS record
 };
 
+// One LDS tile of partners for the first NR row slots of a wave (NR is the
+// wave's slot count, dispatched at run time): no per-slot branches, so each
+// partner record is read once for all NR rows and the NR x U independent pair
+// chains interleave.  With U > 1 the U terms of a row are added in j order
+// after they are all evaluated (a term alone is 0 + t: the sum is never -0).
+template <int D, bool REPEL_ONE, int R, int U, int NR>
+__device__ __forceinline__ void rep_tile(const double* tile, int cnt, const double (&xi)[R][D],
+                                         const double (&di)[R], double repel,
+                                         double (&acc)[R][D]) {
+  constexpr int W = Rec<D>::W;
+  int jj = 0;
+  if constexpr (U > 1) {
+    for (; jj + U <= cnt; jj += U) {
+      double t[U][NR][D];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double* xj = &tile[(jj + u) * W];
+        const double dj = tile[(jj + u) * W + D];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
+          rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
+    }
+  }
+  for (; jj < cnt; ++jj) {
+    const double* xj = &tile[jj * W];
+    const double dj = tile[jj * W + D];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+  }
+}
+
+template <int D, bool REPEL_ONE, int R, int U, int NR>
+__device__ __forceinline__ void rep_tile_dispatch(int nr, const double* tile, int cnt,
+                                                  const double (&xi)[R][D], const double (&di)[R],
+                                                  double repel, double (&acc)[R][D]) {
+  if constexpr (NR >= 1) {
+    if (nr == NR) rep_tile<D, REPEL_ONE, R, U, NR>(tile, cnt, xi, di, repel, acc);
+    else rep_tile_dispatch<D, REPEL_ONE, R, U, NR - 1>(nr, tile, cnt, xi, di, repel, acc);
+  }
+}
+
 template <int D, bool REPEL_ONE, int R>
 __global__ void __launch_bounds__(kRepThreads)
 fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict__ X,
@@ -144,70 +195,7 @@ fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict
       // block-uniform: every coordinate of this tile and of the block's rows is
       // in the exact shared-reciprocal domain (ge_math.hpp)
       if (__syncthreads_and(ok)) {
-        int jj = 0;
-        if (nr == R) {
-          // every slot of the wave has rows: no per-slot branches, so the
-          // partner's LDS record is read once and the R rows' independent
-          // chains interleave
-          if constexpr (U == 1) {
-            for (; jj < cnt; ++jj) {
-              const double* xj = &tile[jj * W];
-              const double dj = tile[jj * W + D];
-#pragma unroll
-              for (int r = 0; r < R; ++r) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
-            }
-          } else {
-            for (; jj + U <= cnt; jj += U) {
-              double t[U][R][D];
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
-                const double* xj = &tile[(jj + u) * W];
-                const double dj = tile[(jj + u) * W + D];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-#pragma unroll
-                  for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
-                  rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
-                }
-              }
-#pragma unroll
-              for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-#pragma unroll
-                  for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
-            }
-          }
-        } else if (U > 1) {
-          for (; jj + U <= cnt; jj += U) {
-            double t[U][R][D];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const double* xj = &tile[(jj + u) * W];
-              const double dj = tile[(jj + u) * W + D];
-#pragma unroll
-              for (int r = 0; r < R; ++r) {
-#pragma unroll
-                for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
-                if (r < nr) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
-              }
-            }
-            // in j order; a term alone is 0 + t (sum never -0, see ge_rows.hpp)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-              for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int k = 0; k < D; ++k) acc[r][k] = acc[r][k] + t[u][r][k];
-          }
-        }
-        for (; jj < cnt; ++jj) {
-          const double* xj = &tile[jj * W];
-          const double dj = tile[jj * W + D];
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (r < nr) rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
-        }
+        rep_tile_dispatch<D, REPEL_ONE, R, U, R>(nr, tile, cnt, xi, di, repel, acc);
       } else {
         for (int jj = 0; jj < cnt; ++jj) {
           const double* xj = &tile[jj * W];
