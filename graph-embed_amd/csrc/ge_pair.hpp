@@ -74,9 +74,11 @@ __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __
   double cij = dip1 * djp1;
   if (!REPEL_ONE) cij = cij * repel;
   if (SHARED) {
-    // In-domain s is 0 or >= 2^-504, so sqrt_normal(max(s, 2^-504)) is exact
-    // for s > 0 and < eps for s == 0; max(dis, eps) is the clamp (no NaN here).
-    const double dis = fmax(sqrt_normal(fmax(s, 0x1p-504)), kFaEps);
+    // In-domain s is 0 or >= 2^-504 (>= 2^-767: sqrt_normal is exact).  For
+    // s == 0 (the j == i pair, coincident points) sqrt_normal returns NaN
+    // (rsq(0) = inf, 0 * inf), and fmax returns its non-NaN operand, so dis is
+    // eps exactly as the reference's clamp of sqrt(0) = 0.
+    const double dis = fmax(sqrt_normal(s), kFaEps);
     const double dd = dis * dis;
     const double val = div_by_nz(cij, recip_of(dd));  // cij > 0 in-domain
     const Recip rc = recip_of(dis);
