@@ -1169,10 +1169,11 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
   int per = (rows + blocks - 1) / blocks;
   per = (per + 63) / 64 * 64;
   const int nb = (rows + per - 1) / per;
-  // Row slots per lane.  Measured at C2 size (scripts/shard_tune.py): with
-  // more than 1024 rows per block 8 slots x 1 partner is fastest; below that
-  // 1 slot x 8 partners (R = 8 at 125 K rows: 379 Gpairs/s, R = 1: 469).
-  int R = per > 2 * kRepThreads ? 8 : 1;
+  // Row slots per lane.  Measured at C2 size (scripts/shard_tune.py, rows of
+  // an N-GPU shard): with more than 512 rows per block 8 slots x 1 partner is
+  // fastest (250 K rows: 557 against 542 Gpairs/s for R = 1); at 512 and below
+  // 1 slot x 8 partners (125 K rows: R = 1 541, R = 8 490 Gpairs/s).
+  int R = per > kRepThreads ? 8 : 1;
   if (const char* e = std::getenv("GE_REP_R")) {  // tuning / test override
     const int r = std::atoi(e);
     if (r == 1 || r == 2 || r == 4 || r == 8) R = r;
