@@ -98,7 +98,7 @@ struct Rec {
 // wave's slot count, dispatched at run time): no per-slot branches, so each
 // partner record is read once for all NR rows and the NR x U independent pair
 // chains interleave.  With U > 1 the U terms of a row are added in j order
-// after they are all evaluated (a term alone is 0 + t: the sum is never -0).
+// after they are all evaluated.
 template <int D, bool REPEL_ONE, int R, int U, int NR>
 __device__ __forceinline__ void rep_tile(const double* tile, int cnt, const double (&xi)[R][D],
                                          const double (&di)[R], double repel,
@@ -113,11 +113,7 @@ __device__ __forceinline__ void rep_tile(const double* tile, int cnt, const doub
         const double* xj = &tile[(jj + u) * W];
         const double dj = tile[(jj + u) * W + D];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-#pragma unroll
-          for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
-          rep_pair<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
-        }
+        for (int r = 0; r < NR; ++r) rep_term<D, true, REPEL_ONE>(xi[r], xj, di[r], dj, repel, t[u][r]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -602,7 +598,7 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
         const int jj = min(q, n - 1);
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
-        rep_pair<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t);
+        rep_term<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t);
         if (q >= n)
 #pragma unroll
           for (int k = 0; k < D; ++k) t[k] = 0.0;
@@ -627,7 +623,7 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
           const int jj = min(j, n - 1);
 #pragma unroll
           for (int k = 0; k < D; ++k) t[u][k] = 0.0;
-          rep_pair<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t[u]);
+          rep_term<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t[u]);
           if (j >= n)
 #pragma unroll
             for (int k = 0; k < D; ++k) t[u][k] = 0.0;
@@ -857,7 +853,7 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
         const int jj = min(q, n - 1);
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
-        rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], repel, t);
+        rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], repel, t);
         if (q >= n)
 #pragma unroll
           for (int k = 0; k < D; ++k) t[k] = 0.0;
@@ -930,7 +926,7 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
       const int jj = min(q, n - 1);
 #pragma unroll
       for (int k = 0; k < D; ++k) t[k] = 0.0;
-      rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
+      rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
       if (q >= n)
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
@@ -1032,7 +1028,7 @@ fa_grouped_stream(int n, int rb, int re, const int* __restrict__ ip, const int* 
         const int jj = min(q, cnt - 1);
 #pragma unroll
         for (int k = 0; k < D; ++k) t[k] = 0.0;
-        rep_pair<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
+        rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
         if (q >= cnt)
 #pragma unroll
           for (int k = 0; k < D; ++k) t[k] = 0.0;
@@ -1170,10 +1166,11 @@ void launch_repulsion(hipStream_t s, int mode, int n, int rb, int re, const doub
   per = (per + 63) / 64 * 64;
   const int nb = (rows + per - 1) / per;
   // Row slots per lane.  Measured at C2 size (scripts/shard_tune.py, rows of
-  // an N-GPU shard): with more than 512 rows per block 8 slots x 1 partner is
-  // fastest (250 K rows: 557 against 542 Gpairs/s for R = 1); at 512 and below
-  // 1 slot x 8 partners (125 K rows: R = 1 541, R = 8 490 Gpairs/s).
-  int R = per > kRepThreads ? 8 : 1;
+  // an N-GPU shard): with more than 1024 rows per block 8 slots x 1 partner is
+  // fastest (500 K rows: 581 against 563 Gpairs/s for R = 1); at 1024 and below
+  // 1 slot x 8 partners (250 K rows: R = 1 566, R = 8 551; 125 K rows: R = 1
+  // 565 Gpairs/s).
+  int R = per > 2 * kRepThreads ? 8 : 1;
   if (const char* e = std::getenv("GE_REP_R")) {  // tuning / test override
     const int r = std::atoi(e);
     if (r == 1 || r == 2 || r == 4 || r == 8) R = r;

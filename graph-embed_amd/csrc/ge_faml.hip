@@ -407,12 +407,9 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
 #pragma unroll
               for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-#pragma unroll
-                  for (int k = 0; k < D; ++k) t[u][r][k] = 0.0;
-                  rep_pair<D, true, REPEL_ONE>(xi[r], &tile[(jj + u) * WV], di[r],
+                for (int r = 0; r < R; ++r)
+                  rep_term<D, true, REPEL_ONE>(xi[r], &tile[(jj + u) * WV], di[r],
                                                tile[(jj + u) * WV + D], repel, t[u][r]);
-                }
 #pragma unroll
               for (int u = 0; u < U; ++u)
 #pragma unroll

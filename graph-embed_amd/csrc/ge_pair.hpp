@@ -58,13 +58,14 @@ __device__ __forceinline__ double attraction_mag(double dis, double a, double di
   return c.attract * f;
 }
 
-// Repulsion of j on i (:152-166), accumulated into acc.  e = x_i - x_j equals
-// -(x_j - x_i) up to the sign of zero, and a zero term never changes the sum
-// (see ge_fa.hip); the j == i term is +0 for the same reason.
+// Repulsion of j on i (:152-166): the term added to row i's sum, out[k] =
+// (e_k / dis) * val.  e = x_i - x_j equals -(x_j - x_i) up to the sign of zero,
+// and a zero term never changes the sum (see ge_fa.hip); the j == i term is
+// +-0 for the same reason.
 template <int D, bool SHARED, bool REPEL_ONE>
-__device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __restrict__ xj,
+__device__ __forceinline__ void rep_term(const double (&xi)[D], const double* __restrict__ xj,
                                          double dip1, double djp1, double repel,
-                                         double (&acc)[D]) {
+                                         double (&out)[D]) {
   double e[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) e[k] = xi[k] - xj[k];
@@ -83,13 +84,24 @@ __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __
     const double val = div_by_nz(cij, recip_of(dd));  // cij > 0 in-domain
     const Recip rc = recip_of(dis);
 #pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = acc[k] + div_by_nz(e[k], rc) * val;
+    for (int k = 0; k < D; ++k) out[k] = div_by_nz(e[k], rc) * val;
   } else {
     const double dis = clamp_eps(sqrt(s));
     const double val = cij / (dis * dis);
 #pragma unroll
-    for (int k = 0; k < D; ++k) acc[k] = acc[k] + (e[k] / dis) * val;
+    for (int k = 0; k < D; ++k) out[k] = (e[k] / dis) * val;
   }
+}
+
+// rep_term added to acc.
+template <int D, bool SHARED, bool REPEL_ONE>
+__device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __restrict__ xj,
+                                         double dip1, double djp1, double repel,
+                                         double (&acc)[D]) {
+  double t[D];
+  rep_term<D, SHARED, REPEL_ONE>(xi, xj, dip1, djp1, repel, t);
+#pragma unroll
+  for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[k];
 }
 
 // attraction_mag for linlog == 0 and delta == 1 (the defaults): no log / pow
