@@ -826,9 +826,10 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   }
   // 4 waves per SIMD: more items per wave for the queue to balance (C3 level
   // 0: 961 ms per call against 1091 ms at the full 8 waves per SIMD)
-  int blocks_cu = std::min(4, rep_occupancy(dim, pl->code));
+  const int occ = rep_occupancy(dim, pl->code);
+  int blocks_cu = std::min(4, occ);
   if (const char* e = std::getenv("GE_FAML_BLOCKS_PER_CU"))  // tuning override
-    blocks_cu = std::max(1, std::min(blocks_cu, std::atoi(e)));
+    blocks_cu = std::max(1, std::min(occ, std::atoi(e)));
   pl->rep_blocks = cus * blocks_cu;
   std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
