@@ -397,15 +397,22 @@ int ge_force_atlas_ml(ge_ctx* ctx, int n, const int* ip, const int* ix, const do
 int ge_partition(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx, double cf,
                  int printing, int positive, double stall, int matching, int merge_leaves,
                  ge_hier** out) {
-  (void)ctx;
   return guarded([&] {
     GE_REQUIRE(out, "null argument");
     GE_REQUIRE(n > 0, "empty graph");
     GE_REQUIRE(!merge_leaves, "mergeLeaves is not supported (off by default; buggy in the "
                               "reference, src/partitioner.cpp:1680)");
     ge::check_csr(n, ip, ix, dx);
-    *out = ge::partition_incremental(n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
-                                     matching);
+    *out = nullptr;
+    // with a context: the device path (integer weights, symmetric, ascending rows);
+    // otherwise, or when the input needs it, the host path
+    const char* force_host = std::getenv("GE_PARTITION_HOST");
+    if (ctx && !(force_host && *force_host && *force_host != '0'))
+      *out = ge::partition_device(ctx, n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
+                                  matching);
+    if (!*out)
+      *out = ge::partition_incremental(n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
+                                       matching);
   });
 }
 

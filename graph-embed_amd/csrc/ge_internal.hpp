@@ -134,6 +134,10 @@ void faml_run_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const
                      const ge_fa_params& p);
 ge_hier* partition_incremental(int n, const int* I, const int* J, const double* Dv, double cf,
                                bool printing, bool positive, double stall, int matching);
+// Device path (ge_partition_dev.hip); nullptr when the input needs the host path
+// (non-integer weights, asymmetric A, rows not strictly ascending).
+ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const double* Dv,
+                          double cf, bool printing, bool positive, double stall, int matching);
 void ptap_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
                  int nnz, int m, const int* d_pt_ip, const int* d_pt_ix, ge_csr* out);
 

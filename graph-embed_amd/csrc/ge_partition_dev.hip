@@ -1,0 +1,1006 @@
+// ge_partition_dev.hip -- the coarsening hierarchy (partition::partition,
+// src/partitioner.cpp:1550-1893) on gfx950, bit-exact with the reference.
+//
+// What one round of the reference does, and what it amounts to:
+//
+//  * scan (:1703-1726): every alive vertex i with !notouch[i] (or max_eta = -inf)
+//    takes the neighbour j with the largest eta = 2*(a_ij/T - alpha_i*alpha_j)
+//    over untouched j; the ascending-j walk with strict `>` selects the
+//    smallest j among the maxima.  That is a segmented argmax under the total
+//    order (eta desc, j asc), so any split of a neighbourhood across lanes
+//    reduces to the same (max_eta, max_ind).
+//  * greedy resolve (:1728-1753): in `used` order, i merges with j = max_ind[i]
+//    when neither is touched yet, !(max_eta[i] < max_eta[j]) and (under
+//    positiveMerging) max_eta[i] > 0.  max_eta / max_ind do not change during
+//    the resolve, only the touched flags do, so the resolve is the greedy
+//    matching of the candidate edges (i, max_ind[i]) taken in the order of the
+//    proposer's `used` slot.  That matching is what the parallel "locally
+//    dominant" rounds compute exactly: an edge whose rank is the smallest among
+//    the live edges at both its endpoints is taken, edges touching a taken
+//    vertex die, repeat (the globally smallest live edge is always taken, so the
+//    loop ends).
+//  * contraction (:1756-1779): the round's merges form a matching, so the new
+//    adjacency is the quotient graph with summed weights and
+//    alpha[i'] = alpha[i'] + alpha[j'].  For integer weights every sum is exact
+//    in any order, so lists are rebuilt with hash tables and atomics.  Non-integer
+//    weights keep the host path (ge_partition.cpp), where the += order is the
+//    reference's.
+//  * swap-pop of `used`, union-find, snapshots (:1797-1834): O(merges) per round,
+//    sequential and order-dependent -> on the host, mirrored into the device
+//    rank array (rank[v] = pointer[v]) by uploading only the changed slots.
+//
+// Data on the device: per-vertex neighbour lists (keys int32, weights fp64) in
+// a pool with per-vertex offset / length / capacity.  Lists keep no order
+// (the scan is order-free) and no duplicate keys (so the list length is the
+// reference's map size, which orients each merge, :1737-1743).
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+#include "ge_internal.hpp"
+
+namespace ge {
+namespace {
+
+constexpr int kNone = 0x7F7F7F7F;  // lock sentinel (memset byte 0x7F), above every rank
+constexpr int kSmallLen = 16;      // scan: one thread per vertex up to this many entries
+constexpr int kMidLen = 4096;      // scan: one wave per vertex up to this many entries
+constexpr int kWaveNeed = 64;      // rebuild: one wave (128-slot LDS table) up to this
+constexpr int kBlockNeed = 2048;   // rebuild: one block (4096-slot LDS table) up to this
+constexpr int kBlockSlots = 4096;
+
+enum {
+  C_MID,
+  C_BIG,
+  C_PROP,
+  C_CAND,
+  C_MERGE,
+  C_DIRTY,
+  C_W,
+  C_B,
+  C_G,
+  C_OVF,
+  C_BAD,  // eligibility flags
+  NCNT
+};
+
+struct MergeRec {
+  int keep, gone, rank, pass;
+  double eta;
+  int len_keep, len_gone;
+};
+
+struct Dev {
+  int N;
+  int positive;
+  double T;
+  int* akey;
+  double* aw;
+  long long* aoff;
+  int* alen;
+  int* acap;
+  double* alpha;
+  int* alive;
+  int* touched;
+  int* rank;
+  double* best;
+  int* arg;
+  int* rep;
+  int* partner;
+  int* dirty;
+  int* lk;
+  int* mid;
+  int* big;
+  int* prop;
+  int* cand;
+  int* cand2;
+  int* cnt;
+  MergeRec* mrec;
+  int* dlist;
+  int* lw;
+  int* lb;
+  int* lg;
+  long long* gofs;
+  int* gmask;
+  int* gkey;
+  double* gw;
+  unsigned long long* gtop;
+  unsigned long long* pool_top;
+  long long pool_cap;
+};
+
+__device__ inline int lane_id() { return threadIdx.x & 63; }
+
+// Append `value` to list[] when pred (one atomic per wave).  Every lane of the
+// wave that is still running must call it.
+__device__ inline void wave_append(int* list, int* counter, bool pred, int value) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return;
+  const int lane = lane_id();
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  if (pred) list[base + __popcll(m & ((1ull << lane) - 1ull))] = value;
+}
+
+// (eta desc, index asc): the reference's ascending walk with strict `>`
+__device__ inline bool better(double e, int k, double be, int bk) {
+  return e > be || (e == be && k < bk);
+}
+
+__device__ inline int agent_load(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline double eta_of(const Dev& d, double w, double au, int k) {
+  return 2.0 * (w / d.T - au * d.alpha[k]);  // :1715 (no contraction: -ffp-contract=off)
+}
+
+__device__ inline bool scan_wanted(const Dev& d, int u) {
+  return d.alive[u] && (!d.touched[u] || d.best[u] == -INFINITY);  // :1706
+}
+
+__device__ inline void scan_store(const Dev& d, int u, double be, int bk, bool& prop) {
+  d.best[u] = be;
+  d.arg[u] = bk == INT_MAX ? -1 : bk;
+  prop = bk != INT_MAX && (!d.positive || be > 0.0);
+}
+
+// ---- scan (:1703-1726) -----------------------------------------------------
+__global__ void scan_small_kernel(Dev d, int pass) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  bool to_mid = false, prop = false;
+  if (u < d.N && scan_wanted(d, u)) {
+    const int len = d.alen[u];
+    if (len > kSmallLen) {
+      to_mid = true;
+    } else {
+      double be = -INFINITY;
+      int bk = INT_MAX;
+      const double au = d.alpha[u];
+      const long long o = d.aoff[u];
+      for (int t = 0; t < len; ++t) {
+        const int k = d.akey[o + t];
+        if (pass > 0 && d.touched[k]) continue;
+        const double e = eta_of(d, d.aw[o + t], au, k);
+        if (better(e, k, be, bk)) {
+          be = e;
+          bk = k;
+        }
+      }
+      scan_store(d, u, be, bk, prop);
+    }
+  }
+  wave_append(d.mid, &d.cnt[C_MID], to_mid, u);
+  wave_append(d.prop, &d.cnt[C_PROP], prop, u);
+}
+
+// Scan entries [b, e) of u's list with `stride` cooperating threads, 4 in flight.
+__device__ inline void scan_range(const Dev& d, int pass, int u, int b, int e, int stride,
+                                  double& be, int& bk) {
+  const double au = d.alpha[u];
+  const long long o = d.aoff[u];
+  int t = b;
+  for (; t + 3 * stride < e; t += 4 * stride) {
+    int k[4];
+    double w[4], a[4];
+    int tc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      k[q] = d.akey[o + t + q * stride];
+      w[q] = d.aw[o + t + q * stride];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = d.alpha[k[q]];
+      tc[q] = pass > 0 ? d.touched[k[q]] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (tc[q]) continue;
+      const double eta = 2.0 * (w[q] / d.T - au * a[q]);
+      if (better(eta, k[q], be, bk)) {
+        be = eta;
+        bk = k[q];
+      }
+    }
+  }
+  for (; t < e; t += stride) {
+    const int k = d.akey[o + t];
+    if (pass > 0 && d.touched[k]) continue;
+    const double eta = eta_of(d, d.aw[o + t], au, k);
+    if (better(eta, k, be, bk)) {
+      be = eta;
+      bk = k;
+    }
+  }
+}
+
+__device__ inline void wave_argmax(double& be, int& bk) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double e2 = __shfl_xor(be, o);
+    const int k2 = __shfl_xor(bk, o);
+    if (better(e2, k2, be, bk)) {
+      be = e2;
+      bk = k2;
+    }
+  }
+}
+
+// one wave per vertex of the mid list; longer lists go on to the big list
+__global__ void scan_mid_kernel(Dev d, int pass) {
+  const int lane = lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int count = d.cnt[C_MID];
+  for (int x = wave; x < count; x += nw) {
+    const int u = d.mid[x];
+    const int len = d.alen[u];
+    if (len > kMidLen) {
+      if (lane == 0) d.big[atomicAdd(&d.cnt[C_BIG], 1)] = u;
+      continue;
+    }
+    double be = -INFINITY;
+    int bk = INT_MAX;
+    scan_range(d, pass, u, lane, len, 64, be, bk);
+    wave_argmax(be, bk);
+    if (lane == 0) {
+      bool prop;
+      scan_store(d, u, be, bk, prop);
+      if (prop) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
+    }
+  }
+}
+
+// one 1024-thread block per vertex of the big list (hubs)
+__global__ void __launch_bounds__(1024) scan_big_kernel(Dev d, int pass) {
+  __shared__ double se[16];
+  __shared__ int sk[16];
+  const int count = d.cnt[C_BIG];
+  const int tid = threadIdx.x;
+  for (int x = blockIdx.x; x < count; x += gridDim.x) {
+    const int u = d.big[x];
+    const int len = d.alen[u];
+    double be = -INFINITY;
+    int bk = INT_MAX;
+    scan_range(d, pass, u, tid, len, blockDim.x, be, bk);
+    wave_argmax(be, bk);
+    if (lane_id() == 0) {
+      se[tid >> 6] = be;
+      sk[tid >> 6] = bk;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      be = tid < (int)(blockDim.x >> 6) ? se[tid] : -INFINITY;
+      bk = tid < (int)(blockDim.x >> 6) ? sk[tid] : INT_MAX;
+      wave_argmax(be, bk);
+      if (tid == 0) {
+        bool prop;
+        scan_store(d, u, be, bk, prop);
+        if (prop) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- resolve (:1728-1753) ---------------------------------------------------
+// candidate edges: untouched i, untouched j = max_ind[i], !(max_eta[i] < max_eta[j])
+__global__ void filter_kernel(Dev d) {
+  const int count = d.cnt[C_PROP];
+  const int stride = gridDim.x * blockDim.x;
+  const int first = blockIdx.x * blockDim.x + threadIdx.x;
+  // uniform trip count per wave (wave_append needs every lane)
+  const int rounds = (count + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = first + r * stride;
+    bool c = false;
+    int i = 0;
+    if (x < count) {
+      i = d.prop[x];
+      const int j = d.arg[i];
+      c = !d.touched[i] && !d.touched[j] && !(d.best[i] < d.best[j]);
+    }
+    wave_append(d.cand, &d.cnt[C_CAND], c, i);
+  }
+}
+
+// Greedy matching in rank order via locally-dominant rounds; one block.
+__global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass) {
+  __shared__ int s_live;
+  int* cur = d.cand;
+  int* nxt = d.cand2;
+  int n = d.cnt[C_CAND];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  int iters = 0;
+  while (n > 0) {
+    if (++iters > (1 << 22)) {  // cannot happen: the smallest live rank is taken every round
+      if (tid == 0) atomicExch(&d.cnt[C_OVF], 2);
+      break;
+    }
+    for (int c = tid; c < n; c += nt) {
+      const int i = cur[c];
+      const int j = d.arg[i];
+      const int r = d.rank[i];
+      atomicMin(&d.lk[i], r);
+      atomicMin(&d.lk[j], r);
+    }
+    if (tid == 0) s_live = 0;
+    __threadfence();  // the L2 atomics are complete before any lane reads lk
+    __syncthreads();
+    for (int c = tid; c < n; c += nt) {
+      const int i = cur[c];
+      const int j = d.arg[i];
+      const int r = d.rank[i];
+      if (agent_load(&d.lk[i]) == r && agent_load(&d.lk[j]) == r) {
+        // :1737-1743: the larger map keeps (ties: the proposer i)
+        const int li = d.alen[i], lj = d.alen[j];
+        MergeRec m;
+        if (li < lj) {
+          m.keep = j;
+          m.gone = i;
+          m.len_keep = lj;
+          m.len_gone = li;
+        } else {
+          m.keep = i;
+          m.gone = j;
+          m.len_keep = li;
+          m.len_gone = lj;
+        }
+        m.rank = r;
+        m.pass = pass;
+        m.eta = d.best[i];
+        d.mrec[atomicAdd(&d.cnt[C_MERGE], 1)] = m;
+        d.touched[i] = 1;
+        d.touched[j] = 1;
+      }
+    }
+    __threadfence();
+    __syncthreads();
+    for (int c = tid; c < n; c += nt) {
+      const int i = cur[c];
+      const int j = d.arg[i];
+      atomicExch(&d.lk[i], kNone);
+      atomicExch(&d.lk[j], kNone);
+      if (!d.touched[i] && !d.touched[j]) nxt[atomicAdd(&s_live, 1)] = i;
+    }
+    __threadfence();
+    __syncthreads();
+    n = s_live;
+    int* t = cur;
+    cur = nxt;
+    nxt = t;
+    __syncthreads();
+  }
+}
+
+// ---- contraction (:1756-1779) -----------------------------------------------
+__global__ void merge_apply_kernel(Dev d) {
+  const int count = d.cnt[C_MERGE];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (count + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    bool ok = x < count;
+    int keep = 0;
+    if (ok) {
+      const MergeRec m = d.mrec[x];
+      keep = m.keep;
+      d.rep[m.gone] = keep;
+      d.alive[m.gone] = 0;
+      d.alpha[keep] = d.alpha[keep] + d.alpha[m.gone];  // :1770
+      d.partner[keep] = m.gone;
+      d.dirty[keep] = 1;
+      d.touched[keep] = 0;  // :1830
+      d.touched[m.gone] = 0;
+    }
+    wave_append(d.dlist, &d.cnt[C_DIRTY], ok, keep);
+  }
+}
+
+// every alive neighbour of an absorbed vertex gets a renamed entry: dirty
+__global__ void mark_dirty_kernel(Dev d) {
+  const int lane = lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int count = d.cnt[C_MERGE];
+  for (int x = wave; x < count; x += nw) {
+    const int keep = d.mrec[x].keep, gone = d.mrec[x].gone;
+    const int len = d.alen[gone];
+    const long long o = d.aoff[gone];
+    for (int b = 0; b < len; b += 64) {
+      const int t = b + lane;
+      bool mk = false;
+      int k = 0;
+      if (t < len) {
+        k = d.akey[o + t];
+        mk = k != keep && d.rep[k] == k && atomicCAS(&d.dirty[k], 0, 1) == 0;
+      }
+      wave_append(d.dlist, &d.cnt[C_DIRTY], mk, k);
+    }
+  }
+}
+
+__device__ inline unsigned pow2_at_least(unsigned x) {
+  unsigned p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+__global__ void classify_kernel(Dev d) {
+  const int count = d.cnt[C_DIRTY];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (count + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    int u = 0, need = 0;
+    if (x < count) {
+      u = d.dlist[x];
+      const int g = d.partner[u];
+      need = d.alen[u] + (g >= 0 ? d.alen[g] : 0);
+    }
+    const bool w = x < count && need <= kWaveNeed;
+    const bool b = x < count && need > kWaveNeed && need <= kBlockNeed;
+    wave_append(d.lw, &d.cnt[C_W], w, u);
+    wave_append(d.lb, &d.cnt[C_B], b, u);
+    if (x < count && need > kBlockNeed) {
+      const unsigned slots = pow2_at_least(2u * (unsigned)need);
+      const int at = atomicAdd(&d.cnt[C_G], 1);
+      d.lg[at] = u;
+      d.gofs[at] = (long long)atomicAdd(d.gtop, (unsigned long long)slots);
+      d.gmask[at] = (int)slots - 1;
+    }
+  }
+}
+
+template <class T>
+__device__ inline T tab_load(T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ inline unsigned slot_hash(int k) { return (unsigned)k * 2654435761u; }
+
+// Rebuild u's list as sum_{members} (rep(k), w), dropping rep(k) == u, into a
+// hash table (LDS or global) of mask+1 slots shared by `nt` threads; then write
+// it back in place (fits) or to fresh pool space.
+template <class Key, class W>
+__device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int tid, int nt,
+                             int* s_cnt, long long* s_dst) {
+  for (int s = tid; s <= mask; s += nt) {
+    tk[s] = -1;
+    tw[s] = 0.0;
+  }
+  if (tid == 0) *s_cnt = 0;
+  __threadfence();
+  __syncthreads();
+  const int g = d.partner[u];
+  for (int m = 0; m < 2; ++m) {
+    const int v = m == 0 ? u : g;
+    if (v < 0) break;
+    const int len = d.alen[v];
+    const long long o = d.aoff[v];
+    for (int t = tid; t < len; t += nt) {
+      const int r = d.rep[d.akey[o + t]];
+      if (r == u) continue;  // the merged pair's own edge: into alpha (:1767-1770)
+      const double w = d.aw[o + t];
+      unsigned h = slot_hash(r) & (unsigned)mask;
+      while (true) {
+        const int prev = atomicCAS(&tk[h], -1, r);
+        if (prev == -1 || prev == r) {
+          atomicAdd(&tw[h], w);  // integer weights: exact in any order
+          break;
+        }
+        h = (h + 1) & (unsigned)mask;
+      }
+    }
+  }
+  __threadfence();  // (global tables) the atomics are complete before the table is read
+  __syncthreads();
+  for (int s = tid; s <= mask; s += nt)
+    if (tab_load(&tk[s]) >= 0) atomicAdd(s_cnt, 1);
+  __syncthreads();
+  const int count = *s_cnt;
+  if (tid == 0) {
+    long long dst = d.aoff[u];
+    if (count > d.acap[u]) {
+      const int cap = count + count / 2 + 4;
+      dst = (long long)atomicAdd(d.pool_top, (unsigned long long)cap);
+      if (dst + cap > d.pool_cap) {
+        atomicExch(&d.cnt[C_OVF], 1);
+        dst = -1;
+      } else {
+        d.aoff[u] = dst;
+        d.acap[u] = cap;
+      }
+    }
+    *s_dst = dst;
+    *s_cnt = 0;
+    if (dst >= 0) d.alen[u] = count;
+  }
+  __syncthreads();
+  const long long dst = *s_dst;
+  if (dst >= 0) {
+    for (int s = tid; s <= mask; s += nt) {
+      const int k = tab_load(&tk[s]);
+      if (k >= 0) {
+        const int at = atomicAdd(s_cnt, 1);
+        d.akey[dst + at] = k;
+        d.aw[dst + at] = tab_load(&tw[s]);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(64) rebuild_wave_kernel(Dev d) {
+  __shared__ int tk[2 * kWaveNeed];
+  __shared__ double tw[2 * kWaveNeed];
+  __shared__ int s_cnt;
+  __shared__ long long s_dst;
+  const int count = d.cnt[C_W];
+  for (int x = blockIdx.x; x < count; x += gridDim.x)
+    rebuild_list(d, d.lw[x], tk, tw, 2 * kWaveNeed - 1, threadIdx.x, 64, &s_cnt, &s_dst);
+}
+
+__global__ void __launch_bounds__(256) rebuild_block_kernel(Dev d) {
+  __shared__ int tk[kBlockSlots];
+  __shared__ double tw[kBlockSlots];
+  __shared__ int s_cnt;
+  __shared__ long long s_dst;
+  const int count = d.cnt[C_B];
+  for (int x = blockIdx.x; x < count; x += gridDim.x)
+    rebuild_list(d, d.lb[x], tk, tw, kBlockSlots - 1, threadIdx.x, 256, &s_cnt, &s_dst);
+}
+
+__global__ void __launch_bounds__(1024) rebuild_global_kernel(Dev d) {
+  __shared__ int s_cnt;
+  __shared__ long long s_dst;
+  const int count = d.cnt[C_G];
+  for (int x = blockIdx.x; x < count; x += gridDim.x)
+    rebuild_list(d, d.lg[x], d.gkey + d.gofs[x], d.gw + d.gofs[x], d.gmask[x], threadIdx.x,
+                 (int)blockDim.x, &s_cnt, &s_dst);
+}
+
+__global__ void dirty_reset_kernel(Dev d) {
+  const int count = d.cnt[C_DIRTY];
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < count; x += gridDim.x * blockDim.x) {
+    const int u = d.dlist[x];
+    d.dirty[u] = 0;
+    d.partner[u] = -1;
+  }
+}
+
+__global__ void rank_update_kernel(Dev d, int count, const int2* __restrict__ ch) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < count) d.rank[ch[x].x] = ch[x].y;
+}
+
+// ---- set-up ------------------------------------------------------------------
+// Eligibility (rows strictly ascending -> no duplicate keys; integer weights;
+// A symmetric with equal weights) and the lists: row i minus its diagonal
+// entry (:1569-1571).  One wave per row.
+__global__ void init_lists_kernel(int n, const int* __restrict__ ip, const int* __restrict__ ix,
+                                  const double* __restrict__ dx, Dev d, double* __restrict__ rowsum,
+                                  double* __restrict__ abs_total, double* __restrict__ self_total) {
+  const int lane = lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int i = wave; i < n; i += nw) {
+    const int b = ip[i], e = ip[i + 1];
+    int self = -1;
+    bool bad = false;
+    double s = 0.0, sa = 0.0, sd = 0.0;
+    for (int t = b + lane; t < e; t += 64) {
+      const int j = ix[t];
+      const double w = dx[t];
+      if (j < 0 || j >= n || (t + 1 < e && !(j < ix[t + 1]))) bad = true;
+      if (!(w == trunc(w)) || !(fabs(w) <= 1099511627776.0)) bad = true;  // |w| <= 2^40
+      if (j == i) {
+        self = t;
+        sd += w;
+      } else if (!bad) {
+        // mirror entry (j, i) with the same weight: binary search in row j
+        int lo = ip[j], hi = ip[j + 1] - 1;
+        bool found = false;
+        while (lo <= hi) {
+          const int mid = (lo + hi) >> 1;
+          const int c = ix[mid];
+          if (c == i) {
+            found = dx[mid] == w;
+            break;
+          }
+          if (c < i) lo = mid + 1;
+          else hi = mid - 1;
+        }
+        if (!found) bad = true;
+      }
+      s += w;
+      sa += fabs(w);
+    }
+    if (__ballot(bad)) {
+      if (lane == 0) atomicOr(&d.cnt[C_BAD], 1);
+    }
+    const unsigned long long sm = __ballot(self >= 0);
+    const int sp = sm ? __shfl(self, __ffsll((long long)sm) - 1) : -1;
+    for (int t = b + lane; t < e; t += 64) {
+      if (t == sp) continue;
+      const int o = (sp >= 0 && t > sp) ? t - 1 : t;
+      d.akey[o] = ix[t];
+      d.aw[o] = dx[t];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o);  // integers: exact in any order
+      sa += __shfl_xor(sa, o);
+      sd += __shfl_xor(sd, o);
+    }
+    if (lane == 0) {
+      d.aoff[i] = b;
+      d.alen[i] = (e - b) - (sp >= 0 ? 1 : 0);
+      d.acap[i] = e - b;
+      rowsum[i] = s;
+      atomicAdd(abs_total, sa);
+      if (sd != 0.0) atomicAdd(self_total, sd);
+    }
+  }
+}
+
+__global__ void init_state_kernel(Dev d, const double* __restrict__ rowsum) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.N) return;
+  d.alpha[i] = rowsum[i] / d.T;  // :1595
+  d.alive[i] = 1;
+  d.touched[i] = 0;
+  d.rank[i] = i;
+  d.best[i] = -INFINITY;
+  d.arg[i] = -1;
+  d.rep[i] = i;
+  d.partner[i] = -1;
+  d.dirty[i] = 0;
+}
+
+// compaction of the pool: new capacity per alive list, then copy
+__global__ void compact_size_kernel(Dev d, long long* __restrict__ cap) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.N) cap[i] = d.alive[i] ? (long long)d.alen[i] + d.alen[i] / 4 + 4 : 0;
+}
+
+__global__ void compact_copy_kernel(Dev d, const long long* __restrict__ noff,
+                                    int* __restrict__ nkey, double* __restrict__ nw) {
+  const int lane = lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwv = (gridDim.x * blockDim.x) >> 6;
+  for (int i = wave; i < d.N; i += nwv) {
+    if (!d.alive[i]) continue;
+    const long long o = d.aoff[i], q = noff[i];
+    const int len = d.alen[i];
+    for (int t = lane; t < len; t += 64) {
+      nkey[q + t] = d.akey[o + t];
+      nw[q + t] = d.aw[o + t];
+    }
+    if (lane == 0) {
+      d.aoff[i] = q;
+      d.acap[i] = (int)(noff[i + 1] - q);
+    }
+  }
+}
+
+inline unsigned blocks_for(long long n, int t) { return (unsigned)std::max<long long>(1, (n + t - 1) / t); }
+
+}  // namespace
+
+// Device path of partition::partition.  Returns nullptr (nothing computed) when
+// the input needs the host path: non-integer or too large weights, an
+// asymmetric matrix, or rows that are not strictly ascending.
+ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const double* Dv,
+                          double cf, bool printing, bool positive, double stall, int matching) {
+  DeviceGuard guard(ctx);
+  hipStream_t st = ctx->stream;
+  const bool prof = std::getenv("GE_PROFILE_PARTITION") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  const auto t_start = now();
+  const long long nnz = I[n];
+  // ---- buffers
+  DevBuf<int> d_ip(n + 1), d_ix(std::max<long long>(nnz, 1));
+  DevBuf<double> d_dx(std::max<long long>(nnz, 1));
+  d_ip.upload(I, n + 1, st);
+  d_ix.upload(J, nnz, st);
+  d_dx.upload(Dv, nnz, st);
+  const long long pool_cap = 3 * nnz + 4 * (long long)n + 1024;
+  DevBuf<int> key_a(pool_cap), key_b(pool_cap);
+  DevBuf<double> w_a(pool_cap), w_b(pool_cap);
+  DevBuf<long long> aoff(n + 1), capbuf(n + 1);
+  DevBuf<int> alen(n), acap(n), alive(n), touched(n), rank(n), arg(n), rep(n), partner(n),
+      dirty(n), lk(n), mid(n), big(n), prop(n), cand(n), cand2(n), dlist(n), lw(n), lb(n), lg(n),
+      gmask(n), cnt(NCNT);
+  DevBuf<long long> gofs(n);
+  DevBuf<double> alpha(n), best(n), rowsum(n), sums(2);
+  DevBuf<MergeRec> mrec(n / 2 + 1);
+  const long long gcap = 4 * (nnz + 64) + 2 * (long long)kBlockSlots;
+  DevBuf<int> gkey(gcap);
+  DevBuf<double> gw(gcap);
+  DevBuf<unsigned long long> tops(2);  // [0] pool top, [1] global-table top
+  DevBuf<int2> d_changes(n / 2 + 1);
+
+  Dev d{};
+  d.N = n;
+  d.positive = positive ? 1 : 0;
+  d.akey = key_a.p;
+  d.aw = w_a.p;
+  d.aoff = aoff.p;
+  d.alen = alen.p;
+  d.acap = acap.p;
+  d.alpha = alpha.p;
+  d.alive = alive.p;
+  d.touched = touched.p;
+  d.rank = rank.p;
+  d.best = best.p;
+  d.arg = arg.p;
+  d.rep = rep.p;
+  d.partner = partner.p;
+  d.dirty = dirty.p;
+  d.lk = lk.p;
+  d.mid = mid.p;
+  d.big = big.p;
+  d.prop = prop.p;
+  d.cand = cand.p;
+  d.cand2 = cand2.p;
+  d.cnt = cnt.p;
+  d.mrec = mrec.p;
+  d.dlist = dlist.p;
+  d.lw = lw.p;
+  d.lb = lb.p;
+  d.lg = lg.p;
+  d.gofs = gofs.p;
+  d.gmask = gmask.p;
+  d.gkey = gkey.p;
+  d.gw = gw.p;
+  d.gtop = tops.p + 1;
+  d.pool_top = tops.p;
+  d.pool_cap = pool_cap;
+
+  GE_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * NCNT, st));
+  GE_HIP(hipMemsetAsync(sums.p, 0, sizeof(double) * 2, st));
+  GE_HIP(hipMemsetAsync(lk.p, 0x7F, sizeof(int) * n, st));
+  hipLaunchKernelGGL(init_lists_kernel, dim3(2048), dim3(256), 0, st, n, d_ip.p, d_ix.p, d_dx.p, d,
+                     rowsum.p, sums.p, sums.p + 1);
+  GE_HIP(hipGetLastError());
+  int bad = 0;
+  double h_sums[2];
+  GE_HIP(hipMemcpyAsync(&bad, cnt.p + C_BAD, sizeof(int), hipMemcpyDeviceToHost, st));
+  GE_HIP(hipMemcpyAsync(h_sums, sums.p, sizeof(h_sums), hipMemcpyDeviceToHost, st));
+  GE_HIP(hipStreamSynchronize(st));
+  if (bad || !(h_sums[0] < 4503599627370496.0)) return nullptr;  // sum |w| < 2^52
+  d_ix.release();
+  d_dx.release();
+  d_ip.release();
+  // T = sum of all entries (:1580-1591): exact (integers), any order
+  std::vector<double> h_rowsum(n);
+  rowsum.download(h_rowsum.data(), n, st);
+  GE_HIP(hipStreamSynchronize(st));
+  double T = 0.0;
+  for (int i = 0; i < n; ++i) T += h_rowsum[i];
+  const double d_sum = h_sums[1];
+  d.T = T;
+  hipLaunchKernelGGL(init_state_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, d, rowsum.p);
+  unsigned long long top0 = (unsigned long long)nnz;
+  GE_HIP(hipMemcpyAsync(tops.p, &top0, sizeof(top0), hipMemcpyHostToDevice, st));
+  double Q = 0.0;
+  if (printing) {  // Q = d_sum/T - sum alpha^2, serial (:1601-1605)
+    std::vector<double> h_alpha(n);
+    alpha.download(h_alpha.data(), n, st);
+    GE_HIP(hipStreamSynchronize(st));
+    Q = d_sum / T;
+    for (int i = 0; i < n; ++i) Q += -h_alpha[i] * h_alpha[i];
+  }
+
+  // ---- host mirrors of the order-dependent state (:1610-1620)
+  auto* h = new ge_hier();
+  std::vector<int> used(n), pointer(n), id(n), basis(n);
+  std::iota(used.begin(), used.end(), 0);
+  pointer = id = basis = used;
+  int N = n, M = n, M_prev = M;
+  auto find = [&](int i) {  // :1622-1633
+    int root = i;
+    while (id[root] != root) root = id[root];
+    while (id[i] != root) {
+      const int a = id[i];
+      id[i] = root;
+      i = a;
+    }
+    return root;
+  };
+  auto snap = [&]() {  // :1799-1808 + interpolationMatrix (:29-65)
+    std::vector<int> cntr(M + 1, 0), rowof(basis.size());
+    for (size_t y = 0; y < basis.size(); ++y) {
+      rowof[y] = pointer[find(basis[y])];
+      cntr[rowof[y] + 1]++;
+    }
+    for (int r = 0; r < M; ++r) cntr[r + 1] += cntr[r];
+    std::vector<int> ix(basis.size());
+    std::vector<int> fill(cntr.begin(), cntr.end() - 1);
+    for (size_t y = 0; y < basis.size(); ++y) ix[fill[rowof[y]]++] = (int)y;
+    h->rows.push_back(M);
+    h->cols.push_back(N);
+    h->indptr.push_back(std::move(cntr));
+    h->indices.push_back(std::move(ix));
+  };
+
+  MergeRec* h_mrec = nullptr;
+  int2* h_changes = nullptr;
+  GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_mrec), sizeof(MergeRec) * (n / 2 + 1)));
+  GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_changes), sizeof(int2) * (n / 2 + 1)));
+  struct PinnedFree {
+    void* a;
+    void* b;
+    ~PinnedFree() {
+      (void)hipHostFree(a);
+      (void)hipHostFree(b);
+    }
+  } pinned_free{h_mrec, h_changes};
+  struct {
+    int merges;
+    unsigned long long top;
+  } rb{};
+  int* h_cnt = nullptr;
+  GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_cnt), sizeof(int) * NCNT));
+  struct PinnedCnt {
+    int* p;
+    ~PinnedCnt() { (void)hipHostFree(p); }
+  } pinned_cnt{h_cnt};
+  unsigned long long* h_top = nullptr;
+  GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_top), sizeof(unsigned long long)));
+  struct PinnedTop {
+    unsigned long long* p;
+    ~PinnedTop() { (void)hipHostFree(p); }
+  } pinned_top{h_top};
+
+  const unsigned scan_blocks = blocks_for(n, 256);
+  double t_dev = 0, t_host = 0, t_compact = 0;
+  long long total_merges = 0;
+  int rounds = 0, compactions = 0;
+  std::vector<MergeRec> order;
+  std::vector<int> stamp(n, 0), moved(n / 2 + 1);
+  do {
+    ++rounds;
+    const auto t0 = now();
+    for (int pass = 0; pass < matching; ++pass) {
+      GE_HIP(hipMemsetAsync(cnt.p + C_MID, 0, sizeof(int) * 4, st));  // MID BIG PROP CAND
+      hipLaunchKernelGGL(scan_small_kernel, dim3(scan_blocks), dim3(256), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_mid_kernel, dim3(1024), dim3(256), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_big_kernel, dim3(256), dim3(1024), 0, st, d, pass);
+      hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d, pass);
+    }
+    GE_HIP(hipGetLastError());
+    GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
+    GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    GE_HIP(hipStreamSynchronize(st));
+    rb.merges = h_cnt[C_MERGE];
+    rb.top = *h_top;
+    if (h_cnt[C_OVF])
+      throw Error(GE_ERR_STATE, h_cnt[C_OVF] == 2 ? "partition_device: resolve did not converge"
+                                                  : "partition_device: list pool overflow");
+    const int nm = rb.merges;
+    if (nm > 0) {
+      GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * nm, hipMemcpyDeviceToHost, st));
+      GE_HIP(hipStreamSynchronize(st));
+      // fresh pool space this round needs at most 1.5 x (both lists) + 4 per keeper
+      long long worst = 0;
+      for (int x = 0; x < nm; ++x)
+        worst += (long long)h_mrec[x].len_keep + h_mrec[x].len_gone +
+                 ((long long)h_mrec[x].len_keep + h_mrec[x].len_gone) / 2 + 4;
+      if ((long long)rb.top + worst > pool_cap) {
+        const auto tc = now();
+        ++compactions;
+        hipLaunchKernelGGL(compact_size_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, st, d,
+                           capbuf.p);
+        GE_HIP(hipMemsetAsync(capbuf.p + n, 0, sizeof(long long), st));
+        DevBuf<long long> noff(n + 1);
+        size_t tmp = 0;
+        GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, capbuf.p, noff.p, n + 1, st));
+        DevBuf<unsigned char> scratch(tmp);
+        GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, capbuf.p, noff.p, n + 1, st));
+        int* nkey = (d.akey == key_a.p) ? key_b.p : key_a.p;
+        double* nwt = (d.aw == w_a.p) ? w_b.p : w_a.p;
+        hipLaunchKernelGGL(compact_copy_kernel, dim3(2048), dim3(256), 0, st, d, noff.p, nkey, nwt);
+        GE_HIP(hipGetLastError());
+        GE_HIP(hipMemcpyAsync(tops.p, noff.p + n, sizeof(long long), hipMemcpyDeviceToDevice, st));
+        GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        GE_HIP(hipStreamSynchronize(st));
+        d.akey = nkey;
+        d.aw = nwt;
+        if ((long long)*h_top + worst > pool_cap)
+          throw Error(GE_ERR_STATE, "partition_device: list pool exhausted after compaction");
+        t_compact += secs(tc, now());
+      }
+      // contraction on the device (asynchronous) while the host does the
+      // order-dependent bookkeeping
+      GE_HIP(hipMemsetAsync(cnt.p + C_DIRTY, 0, sizeof(int) * 4, st));  // DIRTY W B G
+      GE_HIP(hipMemsetAsync(tops.p + 1, 0, sizeof(unsigned long long), st));
+      hipLaunchKernelGGL(merge_apply_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(mark_dirty_kernel, dim3(blocks_for(nm, 4)), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(classify_kernel, dim3(1024), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(rebuild_wave_kernel, dim3(8192), dim3(64), 0, st, d);
+      hipLaunchKernelGGL(rebuild_block_kernel, dim3(1024), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(rebuild_global_kernel, dim3(256), dim3(1024), 0, st, d);
+      hipLaunchKernelGGL(dirty_reset_kernel, dim3(1024), dim3(256), 0, st, d);
+      GE_HIP(hipMemsetAsync(cnt.p + C_MERGE, 0, sizeof(int), st));
+      GE_HIP(hipGetLastError());
+    }
+    const auto t1 = now();
+    t_dev += secs(t0, t1);
+    // ---- host: merges in the reference's order (pass, then `used` slot)
+    order.assign(h_mrec, h_mrec + nm);
+    std::sort(order.begin(), order.end(), [](const MergeRec& a, const MergeRec& b) {
+      return a.pass != b.pass ? a.pass < b.pass : a.rank < b.rank;
+    });
+    double dQ = 0.0;
+    for (const auto& m : order) dQ += m.eta;  // :1749
+    Q += dQ;                                  // :1784
+    M_prev = M;
+    if (1.0 * M / N <= cf) {  // :1797-1815 (before this round's swap-pop)
+      snap();
+      basis = used;
+      N = M;
+    }
+    int nch = 0;
+    for (const auto& m : order) {  // :1819-1834
+      const int idx = pointer[m.gone];
+      const int last = used.back();
+      std::swap(used[idx], used.back());
+      used.pop_back();
+      pointer[last] = idx;
+      id[m.gone] = m.keep;
+      --M;
+      if (stamp[last] != rounds) {  // a vertex may move several times: upload its final slot
+        stamp[last] = rounds;
+        moved[nch++] = last;
+      }
+    }
+    for (int x = 0; x < nch; ++x) h_changes[x] = make_int2(moved[x], pointer[moved[x]]);
+    total_merges += nm;
+    if (nch > 0) {
+      GE_HIP(hipMemcpyAsync(d_changes.p, h_changes, sizeof(int2) * nch, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(rank_update_kernel, dim3(blocks_for(nch, 256)), dim3(256), 0, st, d, nch,
+                         d_changes.p);
+      GE_HIP(hipGetLastError());
+    }
+    t_host += secs(t1, now());
+    if (prof && std::getenv("GE_PROFILE_ROUNDS"))
+      std::fprintf(stderr, "round %d alive %d merges %d pool %llu\n", rounds, M, nm, rb.top);
+  } while (1.0 * M / M_prev < stall);  // :1838
+  GE_HIP(hipStreamSynchronize(st));
+  snap();  // :1840-1852
+  if (prof)
+    std::fprintf(stderr,
+                 "partition_device: n=%d nnz=%lld %d rounds %lld merges %.3fs (device rounds "
+                 "%.3fs, host %.3fs, %d compactions %.3fs)\n",
+                 n, nnz, rounds, total_merges, secs(t_start, now()), t_dev, t_host, compactions,
+                 t_compact);
+  if (printing) {  // :1880-1889
+    std::cout << "modularity: " << Q << std::endl;
+    std::cout << "level 0: " << n << " aggregates" << std::endl;
+    for (size_t l = 0; l < h->rows.size(); ++l)
+      std::cout << "level " << l + 1 << ": " << h->rows[l] << " aggregates" << std::endl;
+  }
+  return h;
+}
+
+}  // namespace ge

@@ -201,6 +201,10 @@ class Context:
     def sync(self):
         _check(lib().ge_ctx_sync(self.h))
 
+    # -- partition (device path) ---------------------------------------------
+    def partition(self, A, coarsening_factor, **kw):
+        return partition(A, coarsening_factor, ctx=self, **kw)
+
     # -- ForceAtlas ----------------------------------------------------------
     def force_atlas(self, A, dim, coords=None, iterations=100000, **kw):
         ip, ix, dx = _csr(A)
@@ -381,11 +385,14 @@ def _take_csr(h):
 # -- host-resident entry points (no device needed) ----------------------------
 
 def partition(A, coarsening_factor, printing=False, positive_merging=True, stall=1.0,
-              matching_iterations=2, merge_leaves=False):
-    """Hierarchy of P_T matrices as (indptr, indices, rows, cols) tuples."""
+              matching_iterations=2, merge_leaves=False, ctx=None):
+    """Hierarchy of P_T matrices as (indptr, indices, rows, cols) tuples.  With a
+    Context the hierarchy is built on its device (integer weights, symmetric A);
+    without one, or for other inputs, by the library's host path."""
     ip, ix, dx = _csr(A)
     h = _vp()
-    _check(lib().ge_partition(None, len(ip) - 1, ip, ix, dx, coarsening_factor, int(printing),
+    _check(lib().ge_partition(ctx.h if ctx is not None else None, len(ip) - 1, ip, ix, dx,
+                              coarsening_factor, int(printing),
                               int(positive_merging), stall, matching_iterations,
                               int(merge_leaves), ctypes.byref(h)))
     try:

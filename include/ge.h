@@ -144,7 +144,10 @@ int ge_faml_plan_destroy(ge_faml_plan* plan);
  * printing, positiveMerging, stallStopThreshold, matchingIterations,
  * mergeLeaves) (include/partitioner.hpp:52-53, src/partitioner.cpp:1550-1893).
  * A must be symmetric.  Level l of the result is P_T[l] (rows x cols, one 1.0
- * per column). */
+ * per column).  ctx != NULL builds the hierarchy on the context's device
+ * (graph-embed_amd/csrc/ge_partition_dev.hip) when A has integer weights and
+ * strictly ascending rows; ctx == NULL, other inputs, or GE_PARTITION_HOST=1 take
+ * the host path.  Both give the reference's P_T arrays. */
 int ge_partition(ge_ctx* ctx, int n, const int* indptr, const int* indices,
                  const double* data, double coarsening_factor, int printing,
                  int positive_merging, double stall_stop_threshold,
