@@ -55,12 +55,14 @@ namespace {
 
 constexpr int kNone = 0x7F7F7F7F;  // lock sentinel (memset byte 0x7F), above every rank
 constexpr int kSmallLen = 16;      // scan: one thread per vertex up to this many entries
-constexpr int kMidLen = 4096;      // scan: one wave per vertex up to this many entries
+constexpr int kMidLen = 512;       // scan: one wave per vertex up to this many entries
+constexpr int kBigLen = 16384;     // scan: one 256-thread block up to this, then 1024 threads
 constexpr int kWaveNeed = 64;      // rebuild: one wave (128-slot LDS table) up to this
 constexpr int kBlockNeed = 2048;   // rebuild: one block (4096-slot LDS table) up to this
 constexpr int kBlockSlots = 4096;
 
 enum {
+  C_SMALL,
   C_MID,
   C_BIG,
   C_PROP,
@@ -72,6 +74,9 @@ enum {
   C_G,
   C_OVF,
   C_BAD,  // eligibility flags
+  C_ALIVE2,
+  C_CAND2,
+  C_HUGE,
   NCNT
 };
 
@@ -84,6 +89,7 @@ struct MergeRec {
 struct Dev {
   int N;
   int positive;
+  int incremental;  // all weights > 0: alphas only grow, see classify_scan_kernel
   double T;
   int* akey;
   double* aw;
@@ -100,8 +106,15 @@ struct Dev {
   int* partner;
   int* dirty;
   int* lk;
+  int* alist;   // alive vertices (may hold dead entries until the next compaction)
+  int* alist2;
+  int* late;    // last scan was a pass >= 1 scan (touched neighbours excluded)
+  int* chg;     // round of the last change of the vertex's list or alpha
+  int* kst;     // round in which the vertex last kept a merge (its alpha grew)
+  int* small;
   int* mid;
   int* big;
+  int* huge;
   int* prop;
   int* cand;
   int* cand2;
@@ -135,9 +148,47 @@ __device__ inline void wave_append(int* list, int* counter, bool pred, int value
   if (pred) list[base + __popcll(m & ((1ull << lane) - 1ull))] = value;
 }
 
+// Append `value` to lists[q] where pred[q], q < L, with one global atomic per
+// list per block (a wave-level atomic per list contends at the L2 when every wave
+// of a large grid appends).  Every thread of the block must call it; s: LDS int[2L].
+template <int L>
+__device__ inline void block_append(int* const (&lists)[L], int* const (&ctrs)[L],
+                                    const bool (&pred)[L], int value, int* s) {
+  const int lane = lane_id();
+  if (threadIdx.x < L) s[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long m[L];
+  int woff[L];
+#pragma unroll
+  for (int q = 0; q < L; ++q) {
+    m[q] = __ballot(pred[q]);
+    int o = 0;
+    if (lane == 0 && m[q]) o = atomicAdd(&s[q], __popcll(m[q]));
+    woff[q] = __shfl(o, 0);
+  }
+  __syncthreads();
+  if (threadIdx.x < L && s[threadIdx.x]) s[L + threadIdx.x] = atomicAdd(ctrs[threadIdx.x], s[threadIdx.x]);
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int q = 0; q < L; ++q)
+    if (pred[q]) lists[q][s[L + q] + woff[q] + __popcll(m[q] & below)] = value;
+  __syncthreads();
+}
+
 // (eta desc, index asc): the reference's ascending walk with strict `>`
 __device__ inline bool better(double e, int k, double be, int bk) {
   return e > be || (e == be && k < bk);
+}
+
+// Wait for this wave's outstanding memory operations (vmcnt/lgkmcnt = 0).  Before a
+// __syncthreads() it orders this block's global atomics before the other waves'
+// reads after the barrier -- the workgroup-scope fence of __syncthreads() does not
+// wait for vector memory, and __threadfence() would write back the whole L2.
+__device__ inline void drain() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
 __device__ inline int agent_load(const int* p) {
@@ -148,10 +199,6 @@ __device__ inline double eta_of(const Dev& d, double w, double au, int k) {
   return 2.0 * (w / d.T - au * d.alpha[k]);  // :1715 (no contraction: -ffp-contract=off)
 }
 
-__device__ inline bool scan_wanted(const Dev& d, int u) {
-  return d.alive[u] && (!d.touched[u] || d.best[u] == -INFINITY);  // :1706
-}
-
 __device__ inline void scan_store(const Dev& d, int u, double be, int bk, bool& prop) {
   d.best[u] = be;
   d.arg[u] = bk == INT_MAX ? -1 : bk;
@@ -159,14 +206,67 @@ __device__ inline void scan_store(const Dev& d, int u, double be, int bk, bool& 
 }
 
 // ---- scan (:1703-1726) -----------------------------------------------------
+// Which alive vertices the reference's scan would give a different answer than
+// the one each vertex already holds; those are rescanned, the others keep their
+// (max_eta, max_ind) -- the same values a rescan returns:
+//  * pass 0: a vertex whose list or alpha changed in the last contraction
+//    (chg), whose max_ind kept a merge (its alpha grew, so the eta towards it
+//    fell), or whose last scan excluded touched neighbours (late).  With
+//    positive weights every alpha is positive and only grows, so the eta towards
+//    any other neighbour can only fall (RN rounding is monotone): the argmax and
+//    its eta stay.
+//  * pass >= 1 (:1706, untouched j only at :1712): an untouched vertex whose
+//    max_ind is untouched keeps it -- the max over a subset that holds the old
+//    argmax -- so only those whose max_ind was touched rescan (and touched ones
+//    with max_eta = -inf, the reference's own rule).
+// Vertices that keep their result and have a usable candidate go straight to the
+// proposer list; the rescans are split by list length.
+__global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full) {
+  __shared__ int s_app[6];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (L + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    int u = 0;
+    bool resc = false, keepprop = false;
+    int len = 0;
+    if (x < L) {
+      u = d.alist[x];
+      if (d.alive[u]) {
+        const bool tu = d.touched[u];
+        const int a = d.arg[u];
+        if (pass == 0) {
+          resc = full || !d.incremental || d.chg[u] == round - 1 || d.late[u] ||
+                 (a >= 0 && d.kst[a] == round - 1);
+        } else if (!tu) {
+          resc = !d.incremental || (a >= 0 && d.touched[a]);
+        } else {
+          resc = d.best[u] == -INFINITY;
+        }
+        if (resc) len = d.alen[u];
+        else keepprop = !tu && a >= 0 && (!d.positive || d.best[u] > 0.0);
+      }
+    }
+    int* const lists[3] = {d.small, d.mid, d.prop};
+    int* const ctrs[3] = {&d.cnt[C_SMALL], &d.cnt[C_MID], &d.cnt[C_PROP]};
+    const bool pr[3] = {resc && len <= kSmallLen, resc && len > kSmallLen, keepprop};
+    block_append<3>(lists, ctrs, pr, u, s_app);
+  }
+}
+
+// one thread per vertex of the small list
 __global__ void scan_small_kernel(Dev d, int pass) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  bool to_mid = false, prop = false;
-  if (u < d.N && scan_wanted(d, u)) {
-    const int len = d.alen[u];
-    if (len > kSmallLen) {
-      to_mid = true;
-    } else {
+  __shared__ int s_app[2];
+  const int count = d.cnt[C_SMALL];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (count + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    bool prop = false;
+    int u = 0;
+    if (x < count) {
+      u = d.small[x];
+      const int len = d.alen[u];
       double be = -INFINITY;
       int bk = INT_MAX;
       const double au = d.alpha[u];
@@ -181,10 +281,14 @@ __global__ void scan_small_kernel(Dev d, int pass) {
         }
       }
       scan_store(d, u, be, bk, prop);
+      d.late[u] = pass > 0;
+      prop = prop && !d.touched[u];
     }
+    int* const lists[1] = {d.prop};
+    int* const ctrs[1] = {&d.cnt[C_PROP]};
+    const bool pr[1] = {prop};
+    block_append<1>(lists, ctrs, pr, u, s_app);
   }
-  wave_append(d.mid, &d.cnt[C_MID], to_mid, u);
-  wave_append(d.prop, &d.cnt[C_PROP], prop, u);
 }
 
 // Scan entries [b, e) of u's list with `stride` cooperating threads, 4 in flight.
@@ -241,38 +345,49 @@ __device__ inline void wave_argmax(double& be, int& bk) {
 }
 
 // one wave per vertex of the mid list; longer lists go on to the big list
-__global__ void scan_mid_kernel(Dev d, int pass) {
+__global__ void __launch_bounds__(256) scan_mid_kernel(Dev d, int pass) {
+  __shared__ int s_app[6];
   const int lane = lane_id();
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int wib = threadIdx.x >> 6;  // wave in block (4 waves)
   const int count = d.cnt[C_MID];
-  for (int x = wave; x < count; x += nw) {
-    const int u = d.mid[x];
-    const int len = d.alen[u];
-    if (len > kMidLen) {
-      if (lane == 0) d.big[atomicAdd(&d.cnt[C_BIG], 1)] = u;
-      continue;
+  for (int base = blockIdx.x * 4; base < count; base += gridDim.x * 4) {
+    const int x = base + wib;
+    int u = 0, len = 0;
+    bool prop = false;
+    if (x < count) {
+      u = d.mid[x];
+      len = d.alen[u];
+      if (len <= kMidLen) {
+        double be = -INFINITY;
+        int bk = INT_MAX;
+        scan_range(d, pass, u, lane, len, 64, be, bk);
+        wave_argmax(be, bk);
+        if (lane == 0) {
+          scan_store(d, u, be, bk, prop);
+          d.late[u] = pass > 0;
+          prop = prop && !d.touched[u];
+        }
+      }
     }
-    double be = -INFINITY;
-    int bk = INT_MAX;
-    scan_range(d, pass, u, lane, len, 64, be, bk);
-    wave_argmax(be, bk);
-    if (lane == 0) {
-      bool prop;
-      scan_store(d, u, be, bk, prop);
-      if (prop) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
-    }
+    // appends aggregated per block (same-address atomics from every wave serialise)
+    int* const lists[3] = {d.prop, d.big, d.huge};
+    int* const ctrs[3] = {&d.cnt[C_PROP], &d.cnt[C_BIG], &d.cnt[C_HUGE]};
+    const bool pr[3] = {prop, lane == 0 && x < count && len > kMidLen && len <= kBigLen,
+                        lane == 0 && x < count && len > kBigLen};
+    block_append<3>(lists, ctrs, pr, u, s_app);
   }
 }
 
-// one 1024-thread block per vertex of the big list (hubs)
-__global__ void __launch_bounds__(1024) scan_big_kernel(Dev d, int pass) {
+// one block per vertex of the big (T = 256) or huge (T = 1024) list
+template <int T>
+__global__ void __launch_bounds__(T) scan_big_kernel(Dev d, int pass) {
   __shared__ double se[16];
   __shared__ int sk[16];
-  const int count = d.cnt[C_BIG];
+  const int count = d.cnt[T == 1024 ? C_HUGE : C_BIG];
+  const int* list = T == 1024 ? d.huge : d.big;
   const int tid = threadIdx.x;
   for (int x = blockIdx.x; x < count; x += gridDim.x) {
-    const int u = d.big[x];
+    const int u = list[x];
     const int len = d.alen[u];
     double be = -INFINITY;
     int bk = INT_MAX;
@@ -290,7 +405,8 @@ __global__ void __launch_bounds__(1024) scan_big_kernel(Dev d, int pass) {
       if (tid == 0) {
         bool prop;
         scan_store(d, u, be, bk, prop);
-        if (prop) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
+        d.late[u] = pass > 0;
+        if (prop && !d.touched[u]) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
       }
     }
     __syncthreads();
@@ -300,6 +416,7 @@ __global__ void __launch_bounds__(1024) scan_big_kernel(Dev d, int pass) {
 // ---- resolve (:1728-1753) ---------------------------------------------------
 // candidate edges: untouched i, untouched j = max_ind[i], !(max_eta[i] < max_eta[j])
 __global__ void filter_kernel(Dev d) {
+  __shared__ int s_app[2];
   const int count = d.cnt[C_PROP];
   const int stride = gridDim.x * blockDim.x;
   const int first = blockIdx.x * blockDim.x + threadIdx.x;
@@ -314,61 +431,121 @@ __global__ void filter_kernel(Dev d) {
       const int j = d.arg[i];
       c = !d.touched[i] && !d.touched[j] && !(d.best[i] < d.best[j]);
     }
-    wave_append(d.cand, &d.cnt[C_CAND], c, i);
+    int* const lists[1] = {d.cand};
+    int* const ctrs[1] = {&d.cnt[C_CAND]};
+    const bool pr[1] = {c};
+    block_append<1>(lists, ctrs, pr, i, s_app);
   }
 }
 
-// Greedy matching in rank order via locally-dominant rounds; one block.
-__global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass) {
+__device__ inline void record_merge(const Dev& d, int i, int j, int r, int pass) {
+  // :1737-1743: the larger map keeps (ties: the proposer i)
+  const int li = d.alen[i], lj = d.alen[j];
+  MergeRec m;
+  if (li < lj) {
+    m.keep = j;
+    m.gone = i;
+    m.len_keep = lj;
+    m.len_gone = li;
+  } else {
+    m.keep = i;
+    m.gone = j;
+    m.len_keep = li;
+    m.len_gone = lj;
+  }
+  m.rank = r;
+  m.pass = pass;
+  m.eta = d.best[i];
+  d.mrec[atomicAdd(&d.cnt[C_MERGE], 1)] = m;
+  d.touched[i] = 1;
+  d.touched[j] = 1;
+}
+
+// The first locally-dominant round over the whole grid (most candidates of a
+// late round are leaves pointing at the same hub: one round removes them).
+__global__ void resolve_min_kernel(Dev d) {
+  const int n = d.cnt[C_CAND];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const int i = d.cand[c];
+    const int r = d.rank[i];
+    atomicMin(&d.lk[i], r);
+    atomicMin(&d.lk[d.arg[i]], r);
+  }
+}
+
+__global__ void resolve_select_kernel(Dev d, int pass) {
+  const int n = d.cnt[C_CAND];
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const int i = d.cand[c];
+    const int j = d.arg[i];
+    const int r = d.rank[i];
+    if (d.lk[i] == r && d.lk[j] == r) record_merge(d, i, j, r, pass);
+  }
+}
+
+__global__ void resolve_filter_kernel(Dev d) {
+  __shared__ int s_app[2];
+  const int n = d.cnt[C_CAND];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (n + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    int i = 0;
+    bool live = false;
+    if (c < n) {
+      i = d.cand[c];
+      const int j = d.arg[i];
+      d.lk[i] = kNone;
+      d.lk[j] = kNone;
+      live = !d.touched[i] && !d.touched[j];
+    }
+    int* const lists[1] = {d.cand2};
+    int* const ctrs[1] = {&d.cnt[C_CAND2]};
+    const bool pr[1] = {live};
+    block_append<1>(lists, ctrs, pr, i, s_app);
+  }
+}
+
+constexpr int kLocalCand = 1024;   // LDS phase: candidates
+constexpr int kLocalSlots = 4096;  // LDS phase: endpoint table (load <= 1/2)
+
+// Greedy matching in rank order via locally-dominant rounds; one block.  While
+// more than kLocalCand candidates are live the rounds run on global memory
+// (vertex-indexed lock array); the rest runs in LDS (endpoints hashed to slots).
+__global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass, int cidx) {
   __shared__ int s_live;
+  __shared__ int hk[kLocalSlots];
+  __shared__ int hl[kLocalSlots];
+  __shared__ unsigned char ht[kLocalSlots];
+  __shared__ int ci[kLocalCand], cj[kLocalCand], cr[kLocalCand];
+  __shared__ short si[kLocalCand], sj[kLocalCand];
+  __shared__ short cl[2][kLocalCand];
   int* cur = d.cand;
   int* nxt = d.cand2;
-  int n = d.cnt[C_CAND];
+  int n = d.cnt[cidx];
   const int tid = threadIdx.x, nt = blockDim.x;
   int iters = 0;
-  while (n > 0) {
+  while (n > kLocalCand) {
     if (++iters > (1 << 22)) {  // cannot happen: the smallest live rank is taken every round
       if (tid == 0) atomicExch(&d.cnt[C_OVF], 2);
-      break;
+      return;
     }
     for (int c = tid; c < n; c += nt) {
       const int i = cur[c];
-      const int j = d.arg[i];
       const int r = d.rank[i];
       atomicMin(&d.lk[i], r);
-      atomicMin(&d.lk[j], r);
+      atomicMin(&d.lk[d.arg[i]], r);
     }
     if (tid == 0) s_live = 0;
-    __threadfence();  // the L2 atomics are complete before any lane reads lk
+    drain();  // the L2 atomics are complete before any lane reads lk
     __syncthreads();
     for (int c = tid; c < n; c += nt) {
       const int i = cur[c];
       const int j = d.arg[i];
       const int r = d.rank[i];
-      if (agent_load(&d.lk[i]) == r && agent_load(&d.lk[j]) == r) {
-        // :1737-1743: the larger map keeps (ties: the proposer i)
-        const int li = d.alen[i], lj = d.alen[j];
-        MergeRec m;
-        if (li < lj) {
-          m.keep = j;
-          m.gone = i;
-          m.len_keep = lj;
-          m.len_gone = li;
-        } else {
-          m.keep = i;
-          m.gone = j;
-          m.len_keep = li;
-          m.len_gone = lj;
-        }
-        m.rank = r;
-        m.pass = pass;
-        m.eta = d.best[i];
-        d.mrec[atomicAdd(&d.cnt[C_MERGE], 1)] = m;
-        d.touched[i] = 1;
-        d.touched[j] = 1;
-      }
+      if (agent_load(&d.lk[i]) == r && agent_load(&d.lk[j]) == r) record_merge(d, i, j, r, pass);
     }
-    __threadfence();
+    drain();
     __syncthreads();
     for (int c = tid; c < n; c += nt) {
       const int i = cur[c];
@@ -377,7 +554,7 @@ __global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass) {
       atomicExch(&d.lk[j], kNone);
       if (!d.touched[i] && !d.touched[j]) nxt[atomicAdd(&s_live, 1)] = i;
     }
-    __threadfence();
+    drain();
     __syncthreads();
     n = s_live;
     int* t = cur;
@@ -385,10 +562,66 @@ __global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass) {
     nxt = t;
     __syncthreads();
   }
+  if (n == 0) return;
+  // ---- LDS phase
+  for (int s = tid; s < kLocalSlots; s += nt) {
+    hk[s] = -1;
+    hl[s] = kNone;
+    ht[s] = 0;
+  }
+  __syncthreads();
+  for (int c = tid; c < n; c += nt) {
+    const int i = cur[c];
+    const int j = d.arg[i];
+    ci[c] = i;
+    cj[c] = j;
+    cr[c] = d.rank[i];
+    for (int e = 0; e < 2; ++e) {
+      const int v = e == 0 ? i : j;
+      unsigned h = ((unsigned)v * 2654435761u) & (kLocalSlots - 1);
+      while (true) {
+        const int prev = atomicCAS(&hk[h], -1, v);
+        if (prev == -1 || prev == v) break;
+        h = (h + 1) & (kLocalSlots - 1);
+      }
+      (e == 0 ? si : sj)[c] = (short)h;
+    }
+    cl[0][c] = (short)c;
+  }
+  __syncthreads();
+  int b = 0;
+  while (n > 0) {
+    for (int x = tid; x < n; x += nt) {
+      const int c = cl[b][x];
+      atomicMin(&hl[si[c]], cr[c]);
+      atomicMin(&hl[sj[c]], cr[c]);
+    }
+    if (tid == 0) s_live = 0;
+    __syncthreads();
+    for (int x = tid; x < n; x += nt) {
+      const int c = cl[b][x];
+      if (hl[si[c]] == cr[c] && hl[sj[c]] == cr[c]) {
+        record_merge(d, ci[c], cj[c], cr[c], pass);
+        ht[si[c]] = 1;
+        ht[sj[c]] = 1;
+      }
+    }
+    __syncthreads();
+    for (int x = tid; x < n; x += nt) {
+      const int c = cl[b][x];
+      hl[si[c]] = kNone;
+      hl[sj[c]] = kNone;
+      if (!ht[si[c]] && !ht[sj[c]]) cl[b ^ 1][atomicAdd(&s_live, 1)] = (short)c;
+    }
+    __syncthreads();
+    n = s_live;
+    b ^= 1;
+    __syncthreads();
+  }
 }
 
 // ---- contraction (:1756-1779) -----------------------------------------------
-__global__ void merge_apply_kernel(Dev d) {
+__global__ void merge_apply_kernel(Dev d, int round) {
   const int count = d.cnt[C_MERGE];
   const int stride = gridDim.x * blockDim.x;
   const int rounds = (count + stride - 1) / stride;
@@ -403,6 +636,7 @@ __global__ void merge_apply_kernel(Dev d) {
       d.alive[m.gone] = 0;
       d.alpha[keep] = d.alpha[keep] + d.alpha[m.gone];  // :1770
       d.partner[keep] = m.gone;
+      d.kst[keep] = round;
       d.dirty[keep] = 1;
       d.touched[keep] = 0;  // :1830
       d.touched[m.gone] = 0;
@@ -484,7 +718,7 @@ __device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int 
     tw[s] = 0.0;
   }
   if (tid == 0) *s_cnt = 0;
-  __threadfence();
+  drain();
   __syncthreads();
   const int g = d.partner[u];
   for (int m = 0; m < 2; ++m) {
@@ -507,10 +741,13 @@ __device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int 
       }
     }
   }
-  __threadfence();  // (global tables) the atomics are complete before the table is read
+  drain();  // (global tables) the atomics are complete before the table is read
   __syncthreads();
-  for (int s = tid; s <= mask; s += nt)
-    if (tab_load(&tk[s]) >= 0) atomicAdd(s_cnt, 1);
+  for (int s0 = 0; s0 <= mask; s0 += nt) {  // used slots, one LDS atomic per wave
+    const int s = s0 + tid;
+    const unsigned long long m = __ballot(s <= mask && tab_load(&tk[s]) >= 0);
+    if (lane_id() == 0 && m) atomicAdd(s_cnt, __popcll(m));
+  }
   __syncthreads();
   const int count = *s_cnt;
   if (tid == 0) {
@@ -533,10 +770,15 @@ __device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int 
   __syncthreads();
   const long long dst = *s_dst;
   if (dst >= 0) {
-    for (int s = tid; s <= mask; s += nt) {
-      const int k = tab_load(&tk[s]);
+    for (int s0 = 0; s0 <= mask; s0 += nt) {
+      const int s = s0 + tid;
+      const int k = s <= mask ? tab_load(&tk[s]) : -1;
+      const unsigned long long m = __ballot(k >= 0);
+      int base = 0;
+      if (lane_id() == 0 && m) base = atomicAdd(s_cnt, __popcll(m));
+      base = __shfl(base, 0);
       if (k >= 0) {
-        const int at = atomicAdd(s_cnt, 1);
+        const int at = base + __popcll(m & ((1ull << lane_id()) - 1ull));
         d.akey[dst + at] = k;
         d.aw[dst + at] = tab_load(&tw[s]);
       }
@@ -561,8 +803,13 @@ __global__ void __launch_bounds__(256) rebuild_block_kernel(Dev d) {
   __shared__ int s_cnt;
   __shared__ long long s_dst;
   const int count = d.cnt[C_B];
-  for (int x = blockIdx.x; x < count; x += gridDim.x)
-    rebuild_list(d, d.lb[x], tk, tw, kBlockSlots - 1, threadIdx.x, 256, &s_cnt, &s_dst);
+  for (int x = blockIdx.x; x < count; x += gridDim.x) {
+    const int u = d.lb[x];
+    const int g = d.partner[u];
+    const int need = d.alen[u] + (g >= 0 ? d.alen[g] : 0);
+    const int slots = (int)pow2_at_least(2u * (unsigned)need);  // <= kBlockSlots
+    rebuild_list(d, u, tk, tw, slots - 1, threadIdx.x, 256, &s_cnt, &s_dst);
+  }
 }
 
 __global__ void __launch_bounds__(1024) rebuild_global_kernel(Dev d) {
@@ -574,12 +821,28 @@ __global__ void __launch_bounds__(1024) rebuild_global_kernel(Dev d) {
                  (int)blockDim.x, &s_cnt, &s_dst);
 }
 
-__global__ void dirty_reset_kernel(Dev d) {
+__global__ void dirty_reset_kernel(Dev d, int round) {
   const int count = d.cnt[C_DIRTY];
   for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < count; x += gridDim.x * blockDim.x) {
     const int u = d.dlist[x];
     d.dirty[u] = 0;
     d.partner[u] = -1;
+    d.chg[u] = round;
+  }
+}
+
+__global__ void alive_compact_kernel(Dev d, int L) {
+  __shared__ int s_app[2];
+  const int stride = gridDim.x * blockDim.x;
+  const int rounds = (L + stride - 1) / stride;
+  for (int r = 0; r < rounds; ++r) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
+    int u = 0;
+    if (x < L) u = d.alist[x];
+    int* const lists[1] = {d.alist2};
+    int* const ctrs[1] = {&d.cnt[C_ALIVE2]};
+    const bool pr[1] = {x < L && d.alive[u]};
+    block_append<1>(lists, ctrs, pr, u, s_app);
   }
 }
 
@@ -670,6 +933,10 @@ __global__ void init_state_kernel(Dev d, const double* __restrict__ rowsum) {
   d.rep[i] = i;
   d.partner[i] = -1;
   d.dirty[i] = 0;
+  d.alist[i] = i;
+  d.late[i] = 0;
+  d.chg[i] = -1;
+  d.kst[i] = -1;
 }
 
 // compaction of the pool: new capacity per alive list, then copy
@@ -726,8 +993,8 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DevBuf<int> key_a(pool_cap), key_b(pool_cap);
   DevBuf<double> w_a(pool_cap), w_b(pool_cap);
   DevBuf<long long> aoff(n + 1), capbuf(n + 1);
-  DevBuf<int> alen(n), acap(n), alive(n), touched(n), rank(n), arg(n), rep(n), partner(n),
-      dirty(n), lk(n), mid(n), big(n), prop(n), cand(n), cand2(n), dlist(n), lw(n), lb(n), lg(n),
+  DevBuf<int> huge(n), alen(n), acap(n), alive(n), touched(n), rank(n), arg(n), rep(n), partner(n),
+      dirty(n), lk(n), alist(n), alist2(n), late(n), chg(n), kst(n), small(n), mid(n), big(n), prop(n), cand(n), cand2(n), dlist(n), lw(n), lb(n), lg(n),
       gmask(n), cnt(NCNT);
   DevBuf<long long> gofs(n);
   DevBuf<double> alpha(n), best(n), rowsum(n), sums(2);
@@ -741,6 +1008,8 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   Dev d{};
   d.N = n;
   d.positive = positive ? 1 : 0;
+  // incremental scans need every alpha > 0 and growing: all weights positive
+  d.incremental = std::getenv("GE_PARTITION_FULL_SCANS") == nullptr;
   d.akey = key_a.p;
   d.aw = w_a.p;
   d.aoff = aoff.p;
@@ -756,8 +1025,15 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d.partner = partner.p;
   d.dirty = dirty.p;
   d.lk = lk.p;
+  d.alist = alist.p;
+  d.alist2 = alist2.p;
+  d.late = late.p;
+  d.chg = chg.p;
+  d.kst = kst.p;
+  d.small = small.p;
   d.mid = mid.p;
   d.big = big.p;
+  d.huge = huge.p;
   d.prop = prop.p;
   d.cand = cand.p;
   d.cand2 = cand2.p;
@@ -787,6 +1063,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   GE_HIP(hipMemcpyAsync(h_sums, sums.p, sizeof(h_sums), hipMemcpyDeviceToHost, st));
   GE_HIP(hipStreamSynchronize(st));
   if (bad || !(h_sums[0] < 4503599627370496.0)) return nullptr;  // sum |w| < 2^52
+  {
+    bool pos = true;
+    for (long long e = 0; e < nnz && pos; ++e) pos = Dv[e] > 0.0;
+    if (!pos) d.incremental = 0;
+  }
   d_ix.release();
   d_dx.release();
   d_ip.release();
@@ -871,28 +1152,47 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     ~PinnedTop() { (void)hipHostFree(p); }
   } pinned_top{h_top};
 
-  const unsigned scan_blocks = blocks_for(n, 256);
+  int alist_len = n;
   double t_dev = 0, t_host = 0, t_compact = 0;
   long long total_merges = 0;
   int rounds = 0, compactions = 0;
   std::vector<MergeRec> order;
   std::vector<int> stamp(n, 0), moved(n / 2 + 1);
+  long long stat[NCNT] = {0};
   do {
     ++rounds;
     const auto t0 = now();
     for (int pass = 0; pass < matching; ++pass) {
-      GE_HIP(hipMemsetAsync(cnt.p + C_MID, 0, sizeof(int) * 4, st));  // MID BIG PROP CAND
-      hipLaunchKernelGGL(scan_small_kernel, dim3(scan_blocks), dim3(256), 0, st, d, pass);
+      GE_HIP(hipMemsetAsync(cnt.p + C_SMALL, 0, sizeof(int) * 5, st));  // SMALL MID BIG PROP CAND
+      GE_HIP(hipMemsetAsync(cnt.p + C_CAND2, 0, sizeof(int) * 2, st));  // CAND2 HUGE
+      hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
+                         pass, alist_len, rounds, rounds == 1 ? 1 : 0);
+      hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(scan_mid_kernel, dim3(1024), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_big_kernel, dim3(256), dim3(1024), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_big_kernel<256>, dim3(1024), dim3(256), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_big_kernel<1024>, dim3(256), dim3(1024), 0, st, d, pass);
       hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
-      hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d, pass);
+      hipLaunchKernelGGL(resolve_min_kernel, dim3(512), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(resolve_select_kernel, dim3(512), dim3(256), 0, st, d, pass);
+      hipLaunchKernelGGL(resolve_filter_kernel, dim3(512), dim3(256), 0, st, d);
+      {
+        Dev d2 = d;  // the survivors are in cand2
+        std::swap(d2.cand, d2.cand2);
+        hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d2, pass, (int)C_CAND2);
+      }
+      if (prof) {  // per-pass list sizes (extra synchronisation: profiling only)
+        GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
+        GE_HIP(hipStreamSynchronize(st));
+        for (int c = C_SMALL; c <= C_CAND; ++c) stat[c] += h_cnt[c];
+      }
     }
     GE_HIP(hipGetLastError());
     GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
     GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     GE_HIP(hipStreamSynchronize(st));
     rb.merges = h_cnt[C_MERGE];
+    if (prof)
+      for (int c = C_DIRTY; c <= C_G; ++c) stat[c] += h_cnt[c];  // previous round's contraction
     rb.top = *h_top;
     if (h_cnt[C_OVF])
       throw Error(GE_ERR_STATE, h_cnt[C_OVF] == 2 ? "partition_device: resolve did not converge"
@@ -934,13 +1234,13 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       // order-dependent bookkeeping
       GE_HIP(hipMemsetAsync(cnt.p + C_DIRTY, 0, sizeof(int) * 4, st));  // DIRTY W B G
       GE_HIP(hipMemsetAsync(tops.p + 1, 0, sizeof(unsigned long long), st));
-      hipLaunchKernelGGL(merge_apply_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(merge_apply_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, st, d, rounds);
       hipLaunchKernelGGL(mark_dirty_kernel, dim3(blocks_for(nm, 4)), dim3(256), 0, st, d);
       hipLaunchKernelGGL(classify_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(rebuild_wave_kernel, dim3(8192), dim3(64), 0, st, d);
       hipLaunchKernelGGL(rebuild_block_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(rebuild_global_kernel, dim3(256), dim3(1024), 0, st, d);
-      hipLaunchKernelGGL(dirty_reset_kernel, dim3(1024), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(dirty_reset_kernel, dim3(1024), dim3(256), 0, st, d, rounds);
       GE_HIP(hipMemsetAsync(cnt.p + C_MERGE, 0, sizeof(int), st));
       GE_HIP(hipGetLastError());
     }
@@ -982,6 +1282,14 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                          d_changes.p);
       GE_HIP(hipGetLastError());
     }
+    if (alist_len > M + M / 4 + 1024) {  // drop the dead entries of the alive list
+      GE_HIP(hipMemsetAsync(cnt.p + C_ALIVE2, 0, sizeof(int), st));
+      hipLaunchKernelGGL(alive_compact_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st,
+                         d, alist_len);
+      GE_HIP(hipGetLastError());
+      std::swap(d.alist, d.alist2);
+      alist_len = M;
+    }
     t_host += secs(t1, now());
     if (prof && std::getenv("GE_PROFILE_ROUNDS"))
       std::fprintf(stderr, "round %d alive %d merges %d pool %llu\n", rounds, M, nm, rb.top);
@@ -994,6 +1302,12 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                  "%.3fs, host %.3fs, %d compactions %.3fs)\n",
                  n, nnz, rounds, total_merges, secs(t_start, now()), t_dev, t_host, compactions,
                  t_compact);
+  if (prof)
+    std::fprintf(stderr,
+                 "partition_device lists (sums over passes): rescans small %lld mid %lld big %lld, "
+                 "proposers %lld, candidates %lld; dirty %lld (wave %lld block %lld global %lld)\n",
+                 stat[C_SMALL], stat[C_MID], stat[C_BIG], stat[C_PROP], stat[C_CAND], stat[C_DIRTY],
+                 stat[C_W], stat[C_B], stat[C_G]);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;
     std::cout << "level 0: " << n << " aggregates" << std::endl;

@@ -5,9 +5,8 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:-part}
 mkdir -p $OUT
 export GE_PROFILE_PARTITION=1
-GE_PROFILE_ROUNDS=1 timeout -k 10 60 python scripts/_part_rounds.py > $OUT/rounds.log 2>&1; head -12 $OUT/rounds.log
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_partition_device.py -k "not c3_digest" > $OUT/tests.log 2>&1; rc=$?
+  tests/test_partition_device.py > $OUT/tests.log 2>&1; rc=$?
 tail -25 $OUT/tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/partition_dev_check.py 1000000 8000000 --host > $OUT/c3.json 2> $OUT/c3.err || { tail -5 $OUT/c3.err; exit 1; }
