@@ -81,15 +81,17 @@ inline double attraction_magnitude(double dis, double a_ij, double deg_ip1,
 }
 
 // One row of the single-level force pass, include/forceatlas.hpp:148-211.
+// frep != nullptr: the repulsion sums are supplied (the value acc holds after
+// :151-167) and only the attraction, gravity part is evaluated.
 void fa_force_row(int i, int n, const int* I, const int* J, const double* D, int dim,
                   const double* X, const double* deg, const orc_fa_params& p,
-                  double* F_row) {
+                  double* F_row, const double* frep = nullptr) {
   double acc[kMaxDim];
-  for (int k = 0; k < dim; ++k) acc[k] = 0.0;
+  for (int k = 0; k < dim; ++k) acc[k] = frep ? frep[k] : 0.0;
   const double* xi = X + (size_t)i * dim;
   const double dip1 = deg[i] + 1;
   // repulsion: every j != i in ascending j  (:151-167)
-  for (int j = 0; j < n; ++j) {
+  for (int j = 0; j < (frep ? 0 : n); ++j) {
     if (j == i) continue;
     const double* xj = X + (size_t)j * dim;
     const double djp1 = deg[j] + 1;
@@ -208,6 +210,31 @@ int orc_fa_step_rows(int n, const int* I, const int* J, const double* D, int dim
   return 0;
 }
 
+// orc_fa_step_rows with the repulsion sums supplied (Frep: (re - rb) x dim, the
+// value each row's force holds after :151-167) -- the check for
+// ge_fa_plan_attract at sizes whose all-pairs repulsion is out of reach.
+int orc_fa_step_rows_frep(int n, const int* I, const int* J, const double* D, int dim,
+                          const double* X, const double* deg, int rb, int re,
+                          const orc_fa_params* p, const double* Frep, double* Fprev, double* Xn,
+                          int nthreads) {
+  if (dim < 1 || dim > kMaxDim) return 1;
+  set_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int i = rb; i < re; ++i) {
+    double F[kMaxDim];
+    fa_force_row(i, n, I, J, D, dim, X, deg, *p, F, Frep + (size_t)(i - rb) * dim);
+    double x[kMaxDim];
+    for (int k = 0; k < dim; ++k) x[k] = X[(size_t)i * dim + k];
+    double* fp = Fprev + (size_t)(i - rb) * dim;
+    fa_update_vertex(x, F, fp, dim, *p, false);
+    for (int k = 0; k < dim; ++k) {
+      Xn[(size_t)i * dim + k] = x[k];
+      fp[k] = F[k];
+    }
+  }
+  return 0;
+}
+
 int orc_force_atlas(int n, const int* I, const int* J, const double* D, int dim,
                     double* X, int init_random, unsigned seed, int iterations,
                     const orc_fa_params* pp, int nthreads) {
@@ -250,22 +277,27 @@ int orc_force_atlas(int n, const int* I, const int* J, const double* D, int dim,
   return 0;
 }
 
-int orc_force_atlas_ml(int n, const int* I, const int* J, const double* D, int m,
-                       const int* PI, const int* PJ, const int* vA, const double* cA,
-                       const double* rA, double* X, int dim, int iterations,
-                       unsigned seed, const orc_fa_params* pp, int nthreads) {
+// forceAtlasMultilevel for the aggregates aggs[0..n_aggs) (all m when aggs is
+// null).  Single-thread draw order of :340-360: aggregates ascending, members in
+// P_T row order, k ascending -> draw c*dim+k for P_T storage position c, whichever
+// aggregates are evaluated.
+int orc_force_atlas_ml_aggs(int n, const int* I, const int* J, const double* D, int m,
+                            const int* PI, const int* PJ, const int* vA, const double* cA,
+                            const double* rA, double* X, int dim, int iterations,
+                            unsigned seed, const orc_fa_params* pp, const int* aggs,
+                            int n_aggs, int nthreads) {
   if (dim < 1 || dim > kMaxDim) return 1;
   const orc_fa_params p = *pp;
   set_threads(nthreads);
   (void)n;
-  // Single-thread draw order of :340-360: aggregates ascending, members in P_T
-  // row order, k ascending -> draw c*dim+k for P_T storage position c.
   const long long total = (long long)PI[m] * dim;
   std::vector<double> draws(total);
   orc_uniform_stream(seed, total, draws.data());
+  const int na = aggs ? n_aggs : m;
 
 #pragma omp parallel for schedule(dynamic, 1)
-  for (int a = 0; a < m; ++a) {
+  for (int x = 0; x < na; ++x) {
+    const int a = aggs ? aggs[x] : x;
     const int base = PI[a];
     const int s = PI[a + 1] - PI[a];
     const int* v = PJ + base;
@@ -356,6 +388,14 @@ int orc_force_atlas_ml(int n, const int* I, const int* J, const double* D, int m
       }
   }
   return 0;
+}
+
+int orc_force_atlas_ml(int n, const int* I, const int* J, const double* D, int m,
+                       const int* PI, const int* PJ, const int* vA, const double* cA,
+                       const double* rA, double* X, int dim, int iterations,
+                       unsigned seed, const orc_fa_params* pp, int nthreads) {
+  return orc_force_atlas_ml_aggs(n, I, J, D, m, PI, PJ, vA, cA, rA, X, dim, iterations, seed,
+                                 pp, nullptr, 0, nthreads);
 }
 
 // ---------------------------------------------------------------------------

@@ -51,6 +51,15 @@ def lib():
                                          _i32p, _i32p, _f64p, _f64p, _f64p, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_uint, ctypes.POINTER(FaParams),
                                          ctypes.c_int]
+        L.orc_fa_step_rows_frep.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                            _f64p, _f64p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(FaParams), _f64p, _f64p, _f64p,
+                                            ctypes.c_int]
+        L.orc_force_atlas_ml_aggs.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                              _i32p, _i32p, _i32p, _f64p, _f64p, _f64p,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_uint,
+                                              ctypes.POINTER(FaParams), _i32p, ctypes.c_int,
+                                              ctypes.c_int]
         L.orc_partition.restype = ctypes.c_void_p
         L.orc_partition.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_double,
                                     ctypes.c_int, ctypes.c_double, ctypes.c_int]
@@ -139,6 +148,39 @@ def fa_step_rows(A, coords, deg, rb, re, fprev_rows, coords_next, nthreads=0, **
                                 ctypes.byref(p), fprev_rows.reshape(-1), coords_next.reshape(-1),
                                 nthreads)
     assert rc == 0
+
+
+def fa_step_rows_frep(A, coords, deg, rb, re, frep_rows, fprev_rows, coords_next, nthreads=0,
+                      **kw):
+    """fa_step_rows with the rows' repulsion sums supplied (frep_rows)."""
+    ip, ix, dx = _csr(A)
+    p = params(**kw)
+    rc = lib().orc_fa_step_rows_frep(len(ip) - 1, ip, ix, dx, coords.shape[1],
+                                     np.ascontiguousarray(coords).reshape(-1), deg, rb, re,
+                                     ctypes.byref(p), np.ascontiguousarray(frep_rows).reshape(-1),
+                                     fprev_rows.reshape(-1), coords_next.reshape(-1), nthreads)
+    assert rc == 0
+
+
+def force_atlas_ml_aggs(A, PT, vertex_A, coords_A, r_A, dim, aggs, iterations=100, seed=0,
+                        nthreads=0, **kw):
+    """force_atlas_ml evaluated for the aggregates `aggs` only (same draw stream); the
+    rows of other aggregates stay 0."""
+    ip, ix, dx = _csr(A)
+    pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+    pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+    n = len(ip) - 1
+    X = np.zeros((n, dim))
+    p = params(**kw)
+    ag = np.ascontiguousarray(aggs, dtype=np.int32)
+    rc = lib().orc_force_atlas_ml_aggs(n, ip, ix, dx, len(pip) - 1, pip, pix,
+                                       np.ascontiguousarray(vertex_A, dtype=np.int32),
+                                       np.ascontiguousarray(coords_A, dtype=np.float64).reshape(-1),
+                                       np.ascontiguousarray(r_A, dtype=np.float64), X.reshape(-1),
+                                       dim, iterations, seed, ctypes.byref(p), ag, len(ag),
+                                       nthreads)
+    assert rc == 0
+    return X
 
 
 def force_atlas_ml(A, PT, vertex_A, coords_A, r_A, dim, iterations=100, seed=0, nthreads=0,
