@@ -36,6 +36,7 @@
 #include "ge_internal.hpp"
 #include "ge_pair.hpp"
 #include "ge_rows.hpp"
+#include "ge_sym.hpp"
 
 namespace ge {
 namespace {
@@ -710,6 +711,11 @@ struct ge_faml_plan {
   ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
+  // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters
+  bool sym = false;
+  ge::DevBuf<int4> units;
+  ge::DevBuf<int> prog;
+  int nunits = 0, ntiles = 0, sym_blocks = 0;
   double streamed_pairs = 0.0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
   // the size classes are independent: streamed path, large, mid and small
@@ -818,6 +824,42 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
                    [](const Item& x, const Item& y) { return x.work > y.work; });
   std::vector<int2> items;
   for (const Item& it : its) items.push_back(make_int2(it.a, it.r0));
+  // symmetric sweeps: one unit per (aggregate, row tile), in the order of their
+  // earliest start (2A tile-times into the aggregate), larger aggregates first
+  {
+    const char* e = std::getenv("GE_FAML_SYM");
+    pl->sym = !(e && *e == '0');
+  }
+  if (pl->sym && !big.empty()) {
+    struct Unit { int a, A, pb, T; };
+    std::vector<Unit> us;
+    int pb = 0;
+    for (int a : big) {
+      const int T = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
+      for (int A = 0; A < T; ++A) us.push_back({a, A, pb, T});
+      pb += T;
+    }
+    std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
+      return x.A != y.A ? x.A < y.A : x.T > y.T;
+    });
+    std::vector<int4> h_units;
+    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, 0));
+    pl->nunits = (int)h_units.size();
+    pl->ntiles = pb;
+    pl->units.alloc(h_units.size());
+    pl->units.upload(h_units.data(), h_units.size(), st);
+    pl->prog.alloc(std::max(pb, 1));
+    int occ = 1;
+    dispatch_dim(dim, [&](auto Dc) {
+      constexpr int D = decltype(Dc)::value;
+      GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
+    });
+    int bpc = std::min(std::max(occ, 1), 4);
+    if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
+      bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
+    pl->sym_blocks = cus * bpc;
+  }
   pl->R = R;
   pl->code = big_code(R, U);
   for (int a : big) {
@@ -924,8 +966,20 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_rev += 2;
           GE_HIP(hipEventRecord(re[0], ss));
         }
-        launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
-                              pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
+        if (pl->sym) {
+          GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
+          if (c.repel == 1.0)
+            hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
+                               ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+          else
+            hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSymT), 0,
+                               ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+        } else {
+          launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
+                                pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
+        }
         if (re) GE_HIP(hipEventRecord(re[1], ss));
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
                              cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};

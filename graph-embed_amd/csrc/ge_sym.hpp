@@ -1,0 +1,198 @@
+// ge_sym.hpp -- all-pairs repulsion inside an aggregate with every unordered
+// pair evaluated once (include/forceatlas.hpp:394-410 multilevel, :151-167),
+// bit-exact with the reference's per-row serial sums.
+//
+// The term of j on i and the term of i on j are exact negatives:
+// x_j - x_i = -(x_i - x_j) in RN, the squared distance and dis are shared,
+// (deg_i+1)(deg_j+1) is commutative, and a quotient / product of a negated
+// operand is the negated result.  Adding -t equals subtracting t.  So one
+// evaluation of t(i, j) serves row i (+t) and row j (-t); what has to be kept is
+// each row's ORDER of additions: partners ascending.
+//
+// Schedule.  Members are split into tiles of 64.  A wave owns a row tile A and
+// sweeps the columns j >= 64A in ascending order as a systolic array: at step
+// s lane l evaluates the pair (row 64A+l, column s-l), so
+//   * row l's own sum (lane register) receives its partners j > row in order;
+//   * column q's sum travels one lane per step (DPP wave shift), entering lane 0
+//     with the value the rows of earlier tiles left in F and collecting the rows
+//     of this tile in ascending order before it leaves lane 63 back to F.
+// In the diagonal tile, column q's travelling sum (partners < q of the tile,
+// after those of earlier tiles) reaches lane q exactly when that lane starts its
+// own row, and becomes the row's sum.  Row 64A+l therefore adds, in order:
+// partners of tiles < A (sweeps 0..A-1, as a column), partners < itself in tile
+// A (travelling), partners > itself (own sweep) -- the reference's order.
+//
+// Dependencies: the sweep of row tile A may start column tile B only after the
+// sweeps 0..A-1 have written it back (prog[B] == A).  Sweeps are taken from a
+// queue ordered by their earliest possible start (2A tile-times after the
+// aggregate's first sweep): every sweep waits only on sweeps taken before it,
+// which are running, so the persistent grid cannot deadlock.  Column sums are
+// handed over with agent-scope (L2-bypassing) stores and loads: the waves of
+// one aggregate run on different XCDs, whose L2s are not coherent.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ge_pair.hpp"
+#include "ge_rows.hpp"
+
+namespace ge {
+
+constexpr int kSymT = 256;  // threads per block (4 independent waves)
+
+template <int D>
+struct SymW {
+  static constexpr int v = (D + 1 <= 4) ? 4 : 8;  // record: x[D], deg+1, pad
+};
+
+// Wave-wide shift by one lane (DPP wave_shr:1): lane l receives v of lane l-1,
+// lane 0 keeps in0 (no source lane: the DPP move leaves the destination alone).
+__device__ __forceinline__ double wave_shift_in(double v, double in0) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(in0), __double2loint(v), 0x138, 0xF,
+                                             0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(in0), __double2hiint(v), 0x138, 0xF,
+                                             0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double agent_ld(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_st(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// steps [s0, s1) of a sweep; rec/ini: the two LDS tile slots (column records,
+// column sums on entry)
+template <int D, bool SHARED, bool REPEL_ONE>
+__device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int A, int ncols, size_t cbase,
+                                          const double* rec, const double* ini,
+                                          const double (&xr)[D], double dr, bool rv, double repel,
+                                          double (&racc)[D], double (&flow)[D], double* F,
+                                          int* prog) {
+  constexpr int WV = SymW<D>::v;
+  for (int sg = s0; sg < s1; ++sg) {
+    // column sg enters lane 0 with its stored sum (broadcast LDS read)
+    double in0[D];
+    const double* ic = ini + ((sg >> 6) & 1) * 64 * D + (sg & 63) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) in0[k] = sg < ncols ? ic[k] : 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) flow[k] = wave_shift_in(flow[k], in0[k]);
+    const int q = sg - lane;
+    if (q == lane) {  // diagonal tile: the travelling sum becomes the row's own
+#pragma unroll
+      for (int k = 0; k < D; ++k) racc[k] = flow[k];
+    }
+    if (rv && q > lane && q < ncols) {
+      const double* xq = rec + ((q >> 6) & 1) * 64 * WV + (q & 63) * WV;
+      double t[D];
+      rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        racc[k] = racc[k] + t[k];
+        flow[k] = flow[k] - t[k];
+      }
+    }
+    // column sg - 63 leaves lane 63 (diagonal-tile columns end inside the tile)
+    const int qo = sg - 63;
+    if (qo >= 64 && qo < ncols && lane == 63) {
+      double* fo = F + (cbase + qo) * D;
+#pragma unroll
+      for (int k = 0; k < D; ++k) agent_st(fo + k, flow[k]);
+      if ((qo & 63) == 63 || qo == ncols - 1) {  // the tile's last column: hand it over
+        __builtin_amdgcn_s_waitcnt(0);
+        __hip_atomic_store(prog + (qo >> 6), A + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog, 0}
+// in queue order; prog zeroed before the launch; queue = one counter.
+template <int D, bool REPEL_ONE>
+__global__ void __launch_bounds__(kSymT)
+faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
+                 const int* __restrict__ pt_ip, const double* __restrict__ X,
+                 const double* __restrict__ DP, double repel, double* __restrict__ F,
+                 int* __restrict__ prog) {
+  constexpr int WV = SymW<D>::v;
+  __shared__ __attribute__((aligned(16))) double srec[kSymT / 64][2 * 64 * WV];
+  __shared__ double sini[kSymT / 64][2 * 64 * D];
+  const int lane = threadIdx.x & 63;
+  double* rec = srec[threadIdx.x >> 6];
+  double* ini = sini[threadIdx.x >> 6];
+  const bool repel_ok = REPEL_ONE || weight_ok(repel);
+  for (;;) {
+    int qi = 0;
+    if (lane == 0) qi = atomicAdd(queue, 1);
+    qi = __builtin_amdgcn_readfirstlane(qi);
+    if (qi >= nunits) break;  // every wave leaves once the queue is drained
+    const int4 u = units[qi];
+    const int A = u.y;
+    const int base = pt_ip[u.x];
+    const int s = pt_ip[u.x + 1] - base;
+    int* tprog = prog + u.z + A;  // tprog[t]: column tile A + t
+    const size_t cbase = (size_t)base + 64 * (size_t)A;
+    const bool rv = 64 * A + lane < s;
+    double xr[D], racc[D], flow[D], dr = 1.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
+      racc[k] = 0.0;
+      flow[k] = 0.0;
+    }
+    if (rv) dr = DP[cbase + lane];
+    const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
+    const int ncols = s - 64 * A;
+    const int ntiles = (ncols + 63) >> 6;
+    bool ok_prev = true;
+    for (int tt = 0; tt < ntiles; ++tt) {
+      if (A > 0)  // the sweeps 0..A-1 have written column tile A + tt back
+        while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
+          __builtin_amdgcn_s_sleep(1);
+      const int qc = 64 * tt + lane;
+      const bool cv = qc < ncols;
+      double xc[D], ic[D], dc = 1.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
+        ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
+      }
+      if (cv) dc = DP[cbase + qc];
+      const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
+      double* rs = rec + (tt & 1) * 64 * WV + lane * WV;
+      double* is = ini + (tt & 1) * 64 * D + lane * D;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        rs[k] = xc[k];
+        is[k] = ic[k];
+      }
+      rs[D] = dc;
+      wave_lds_sync();
+      // steps of this tile touch tiles tt-1 and tt
+      if (rows_ok && ok_cur && ok_prev)
+        sym_steps<D, true, REPEL_ONE>(64 * tt, 64 * tt + 64, lane, A, ncols, cbase, rec, ini, xr,
+                                      dr, rv, repel, racc, flow, F, tprog);
+      else
+        sym_steps<D, false, REPEL_ONE>(64 * tt, 64 * tt + 64, lane, A, ncols, cbase, rec, ini,
+                                       xr, dr, rv, repel, racc, flow, F, tprog);
+      ok_prev = ok_cur;
+      wave_lds_sync();  // the slot of tile tt-1 is free for tile tt+1
+    }
+    const int send = ncols + 63;  // drain: the last columns cross the wave
+    if (rows_ok && ok_prev)
+      sym_steps<D, true, REPEL_ONE>(64 * ntiles, send, lane, A, ncols, cbase, rec, ini, xr, dr,
+                                    rv, repel, racc, flow, F, tprog);
+    else
+      sym_steps<D, false, REPEL_ONE>(64 * ntiles, send, lane, A, ncols, cbase, rec, ini, xr, dr,
+                                     rv, repel, racc, flow, F, tprog);
+    if (rv) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
+    }
+    wave_lds_sync();
+  }
+}
+
+}  // namespace ge
