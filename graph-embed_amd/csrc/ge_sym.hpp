@@ -62,66 +62,135 @@ __device__ __forceinline__ void agent_st(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// steps [s0, s1) of a sweep; rec/ini: the two LDS tile slots (column records,
-// column sums on entry)
-template <int D, bool SHARED, bool REPEL_ONE>
-__device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int A, int ncols, size_t cbase,
-                                          const double* rec, const double* ini,
-                                          const double (&xr)[D], double dr, bool rv, double repel,
-                                          double (&racc)[D], double (&flow)[D], double* F,
-                                          int* prog) {
-  constexpr int WV = SymW<D>::v;
-  for (int sg = s0; sg < s1; ++sg) {
-    // column sg enters lane 0 with its stored sum (broadcast LDS read)
-    double in0[D];
-    const double* ic = ini + ((sg >> 6) & 1) * 64 * D + (sg & 63) * D;
+constexpr int kSymRing = 128;  // LDS ring of column slots (column q at q & 127)
+
+template <int D>
+struct SymI {
+  static constexpr int v = D;  // column-sum slot width (3 KB per 128-slot ring at D = 3)
+};
+
+// Steps [s0, s1) of a sweep.  DIAG: the steps may meet the diagonal tile
+// (s < 127), where a lane takes the travelling sum of its own row over.  The LDS
+// reads of step s + 1 (entering column sum, partner record) are issued before
+// step s computes: both were staged before the steps began.
+template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
+__device__ __forceinline__ void sym_step(int sg, int lane, int ncols, double* out,
+                                         const double (&xr)[D], double dr, bool rv, double repel,
+                                         const double (&in0)[D], const double (&xq)[D + 1],
+                                         double (&racc)[D], double (&flow)[D]) {
+  constexpr int IW = SymI<D>::v;
+  // column sg enters lane 0 with its stored sum
 #pragma unroll
-    for (int k = 0; k < D; ++k) in0[k] = sg < ncols ? ic[k] : 0.0;
+  for (int k = 0; k < D; ++k) flow[k] = wave_shift_in(flow[k], in0[k]);
+  if (DIAG && sg - lane == lane) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) flow[k] = wave_shift_in(flow[k], in0[k]);
-    const int q = sg - lane;
-    if (q == lane) {  // diagonal tile: the travelling sum becomes the row's own
-#pragma unroll
-      for (int k = 0; k < D; ++k) racc[k] = flow[k];
-    }
-    if (rv && q > lane && q < ncols) {
-      const double* xq = rec + ((q >> 6) & 1) * 64 * WV + (q & 63) * WV;
-      double t[D];
-      rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        racc[k] = racc[k] + t[k];
-        flow[k] = flow[k] - t[k];
-      }
-    }
-    // column sg - 63 leaves lane 63 (diagonal-tile columns end inside the tile)
-    const int qo = sg - 63;
-    if (qo >= 64 && qo < ncols && lane == 63) {
-      double* fo = F + (cbase + qo) * D;
-#pragma unroll
-      for (int k = 0; k < D; ++k) agent_st(fo + k, flow[k]);
-      if ((qo & 63) == 63 || qo == ncols - 1) {  // the tile's last column: hand it over
-        __builtin_amdgcn_s_waitcnt(0);
-        __hip_atomic_store(prog + (qo >> 6), A + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    for (int k = 0; k < D; ++k) racc[k] = flow[k];
   }
+  // Every lane evaluates a term every step (no divergent exec mask): a pair with
+  // an inert row or column (deg+1 = 0) and the self pair are +-0, which leave a
+  // sum unchanged; below the diagonal (before its own row starts) a lane's racc
+  // and the absorbed columns' sums are dead values.
+  double t[D];
+  rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    racc[k] = racc[k] + t[k];
+    flow[k] = flow[k] - t[k];
+  }
+  if (lane == 63) {  // column sg - 63 leaves the wave
+    double* o = out + ((sg - 63) & (kSymRing - 1)) * IW;
+#pragma unroll
+    for (int k = 0; k < D; ++k) o[k] = flow[k];
+  }
+}
+
+// LDS reads of one step: the entering column sum (broadcast) and the partner record
+template <int D>
+__device__ __forceinline__ void sym_fetch(int sg, int lane, const double* rec, const double* ini,
+                                          double (&i0)[D], double (&xv)[D + 1]) {
+  constexpr int WV = SymW<D>::v;
+  constexpr int IW = SymI<D>::v;
+  const double* ic = ini + (sg & (kSymRing - 1)) * IW;
+  const double* xs = rec + ((sg - lane) & (kSymRing - 1)) * WV;
+#pragma unroll
+  for (int k = 0; k < D; ++k) i0[k] = ic[k];
+#pragma unroll
+  for (int k = 0; k <= D; ++k) xv[k] = xs[k];
+}
+
+// Steps [s0, s1) of a sweep.  DIAG: the steps may meet the diagonal tile
+// (s < 127), where a lane takes the travelling sum of its own row over.  The LDS
+// reads of step s + 1 are issued before step s computes (both slots were staged
+// before the steps began); two register sets alternate.
+template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
+__device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, const double* rec,
+                                          const double* ini, double* out,
+                                          const double (&xr)[D], double dr, bool rv, double repel,
+                                          double (&racc)[D], double (&flow)[D]) {
+  if (s0 >= s1) return;
+  double ia[D], xa[D + 1], ib[D], xb[D + 1];
+  sym_fetch<D>(s0, lane, rec, ini, ia, xa);
+  for (int sg = s0;; sg += 2) {
+    sym_fetch<D>(sg + 1, lane, rec, ini, ib, xb);
+    sym_step<D, SHARED, REPEL_ONE, DIAG>(sg, lane, ncols, out, xr, dr, rv, repel, ia, xa, racc,
+                                         flow);
+    if (sg + 1 >= s1) break;
+    sym_fetch<D>(sg + 2, lane, rec, ini, ia, xa);
+    sym_step<D, SHARED, REPEL_ONE, DIAG>(sg + 1, lane, ncols, out, xr, dr, rv, repel, ib, xb,
+                                         racc, flow);
+    if (sg + 2 >= s1) break;
+  }
+}
+
+// Column tile t of the sweep has left lane 63: write its sums back, then let the
+// next sweep of the aggregate have it.
+template <int D>
+__device__ __forceinline__ void sym_handover(int t, int lane, int A, int ncols, size_t cbase,
+                                             const double* out, double* F, int* tprog) {
+  constexpr int IW = SymI<D>::v;
+  wave_lds_sync();
+  const int qo = 64 * t + lane;
+  if (qo < ncols) {
+    const double* o = out + (qo & (kSymRing - 1)) * IW;
+#pragma unroll
+    for (int k = 0; k < D; ++k) agent_st(F + (cbase + qo) * D + k, o[k]);
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // every lane's sums are stored before the flag
+  if (lane == 0) __hip_atomic_store(tprog + t, A + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int D, bool REPEL_ONE, bool DIAG>
+__device__ __forceinline__ void sym_steps_any(bool fast, int s0, int s1, int lane, int ncols,
+                                              const double* rec, const double* ini, double* out,
+                                              const double (&xr)[D], double dr, bool rv,
+                                              double repel, double (&racc)[D], double (&flow)[D]) {
+  if (fast)
+    sym_steps<D, true, REPEL_ONE, DIAG>(s0, s1, lane, ncols, rec, ini, out, xr, dr, rv, repel,
+                                        racc, flow);
+  else
+    sym_steps<D, false, REPEL_ONE, DIAG>(s0, s1, lane, ncols, rec, ini, out, xr, dr, rv, repel,
+                                         racc, flow);
 }
 
 // units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog, 0}
 // in queue order; prog zeroed before the launch; queue = one counter.
+// 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3)
 template <int D, bool REPEL_ONE>
-__global__ void __launch_bounds__(kSymT)
+__global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
                  int* __restrict__ prog) {
   constexpr int WV = SymW<D>::v;
-  __shared__ __attribute__((aligned(16))) double srec[kSymT / 64][2 * 64 * WV];
-  __shared__ double sini[kSymT / 64][2 * 64 * D];
+  constexpr int IW = SymI<D>::v;
+  constexpr int NW = kSymT / 64;
+  __shared__ __attribute__((aligned(16))) double srec[NW][kSymRing * WV];
+  __shared__ __attribute__((aligned(16))) double sini[NW][kSymRing * IW];
+  __shared__ __attribute__((aligned(16))) double sout[NW][kSymRing * IW];
   const int lane = threadIdx.x & 63;
   double* rec = srec[threadIdx.x >> 6];
   double* ini = sini[threadIdx.x >> 6];
+  double* out = sout[threadIdx.x >> 6];
   const bool repel_ok = REPEL_ONE || weight_ok(repel);
   for (;;) {
     int qi = 0;
@@ -135,7 +204,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     int* tprog = prog + u.z + A;  // tprog[t]: column tile A + t
     const size_t cbase = (size_t)base + 64 * (size_t)A;
     const bool rv = 64 * A + lane < s;
-    double xr[D], racc[D], flow[D], dr = 1.0;
+    double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
@@ -153,7 +222,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
           __builtin_amdgcn_s_sleep(1);
       const int qc = 64 * tt + lane;
       const bool cv = qc < ncols;
-      double xc[D], ic[D], dc = 1.0;
+      double xc[D], ic[D], dc = 0.0;  // a column past the aggregate is inert
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
@@ -161,8 +230,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       }
       if (cv) dc = DP[cbase + qc];
       const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
-      double* rs = rec + (tt & 1) * 64 * WV + lane * WV;
-      double* is = ini + (tt & 1) * 64 * D + lane * D;
+      double* rs = rec + (qc & (kSymRing - 1)) * WV;
+      double* is = ini + (qc & (kSymRing - 1)) * IW;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         rs[k] = xc[k];
@@ -170,23 +239,35 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       }
       rs[D] = dc;
       wave_lds_sync();
-      // steps of this tile touch tiles tt-1 and tt
-      if (rows_ok && ok_cur && ok_prev)
-        sym_steps<D, true, REPEL_ONE>(64 * tt, 64 * tt + 64, lane, A, ncols, cbase, rec, ini, xr,
-                                      dr, rv, repel, racc, flow, F, tprog);
+      // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
+      const bool fast = rows_ok && ok_cur && ok_prev;
+      if (tt < 2)
+        sym_steps_any<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini, out,
+                                          xr, dr, rv, repel, racc, flow);
       else
-        sym_steps<D, false, REPEL_ONE>(64 * tt, 64 * tt + 64, lane, A, ncols, cbase, rec, ini,
-                                       xr, dr, rv, repel, racc, flow, F, tprog);
+        sym_steps_any<D, REPEL_ONE, false>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini,
+                                           out, xr, dr, rv, repel, racc, flow);
       ok_prev = ok_cur;
-      wave_lds_sync();  // the slot of tile tt-1 is free for tile tt+1
+      if (tt >= 2) sym_handover<D>(tt - 1, lane, A, ncols, cbase, out, F, tprog);
+      wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
     }
-    const int send = ncols + 63;  // drain: the last columns cross the wave
-    if (rows_ok && ok_prev)
-      sym_steps<D, true, REPEL_ONE>(64 * ntiles, send, lane, A, ncols, cbase, rec, ini, xr, dr,
-                                    rv, repel, racc, flow, F, tprog);
+    {  // drain: the last columns cross the wave; the slots past them hold inert records
+      double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1)) * WV;
+      double* is = ini + ((64 * ntiles + lane) & (kSymRing - 1)) * IW;
+#pragma unroll
+      for (int k = 0; k <= D; ++k) rs[k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) is[k] = 0.0;
+      wave_lds_sync();
+    }
+    const int s0 = 64 * ntiles, s1 = ncols + 63;
+    if (ntiles < 2)
+      sym_steps_any<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
+                                        xr, dr, rv, repel, racc, flow);
     else
-      sym_steps<D, false, REPEL_ONE>(64 * ntiles, send, lane, A, ncols, cbase, rec, ini, xr, dr,
-                                     rv, repel, racc, flow, F, tprog);
+      sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
+                                         xr, dr, rv, repel, racc, flow);
+    if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A, ncols, cbase, out, F, tprog);
     if (rv) {
 #pragma unroll
       for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
