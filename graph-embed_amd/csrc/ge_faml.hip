@@ -831,24 +831,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     pl->sym = !(e && *e == '0');
   }
   if (pl->sym && !big.empty()) {
-    struct Unit { int a, A, pb, T; };
-    std::vector<Unit> us;
-    int pb = 0;
-    for (int a : big) {
-      const int T = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
-      for (int A = 0; A < T; ++A) us.push_back({a, A, pb, T});
-      pb += T;
-    }
-    std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
-      return x.A != y.A ? x.A < y.A : x.T > y.T;
-    });
-    std::vector<int4> h_units;
-    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, 0));
-    pl->nunits = (int)h_units.size();
-    pl->ntiles = pb;
-    pl->units.alloc(h_units.size());
-    pl->units.upload(h_units.data(), h_units.size(), st);
-    pl->prog.alloc(std::max(pb, 1));
+    // The sweeps of an aggregate with T row tiles form a chain of ~2.5 T tile-times
+    // (each sweep starts after its predecessor has passed its first two tiles); the
+    // launch takes about (sum of T^2 / 2 sweep tiles) / (resident waves).  While the
+    // longest chain exceeds that, the largest aggregate runs as plain row blocks
+    // (every ordered pair, ~0.8 the step cost of a sweep, no chain).
+    std::vector<int> T(big.size());
+    for (size_t b = 0; b < big.size(); ++b) T[b] = (h_pt_ip[big[b] + 1] - h_pt_ip[big[b]] + 63) / 64;
     int occ = 1;
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
@@ -859,6 +848,49 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
+    const double waves = (double)pl->sym_blocks * (kSymT / 64);
+    std::vector<size_t> by_T(big.size());
+    std::iota(by_T.begin(), by_T.end(), 0);
+    std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
+    std::vector<char> rows_mode(big.size(), 0);
+    double work = 0.0;
+    for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
+    double chain_k = 2.5;
+    if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
+    for (size_t r = 0; r < by_T.size() && chain_k > 0.0; ++r) {
+      const size_t b = by_T[r];
+      if (chain_k * T[b] <= work / waves) break;
+      rows_mode[b] = 1;
+      work += 0.8 * T[b] * (double)T[b] - (0.5 * T[b] * (double)T[b] + T[b]);
+    }
+    struct Unit { int a, A, pb, T, kind; double est; };
+    std::vector<Unit> us;
+    int pb = 0;
+    double est_max = 0.0;
+    for (size_t b = 0; b < big.size(); ++b) {
+      if (rows_mode[b]) continue;
+      for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], 0, 2.0 * A});
+      est_max = std::max(est_max, 2.0 * (T[b] - 1));
+      pb += T[b];
+    }
+    std::vector<Unit> rows_units;
+    for (size_t b = 0; b < big.size(); ++b)
+      if (rows_mode[b])
+        for (int A = 0; A < T[b]; ++A) rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
+    for (size_t k = 0; k < rows_units.size(); ++k) {  // spread among the sweeps
+      rows_units[k].est = est_max * (double)k / (double)std::max<size_t>(rows_units.size(), 1);
+      us.push_back(rows_units[k]);
+    }
+    std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
+      return x.est != y.est ? x.est < y.est : x.T > y.T;
+    });
+    std::vector<int4> h_units;
+    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.kind));
+    pl->nunits = (int)h_units.size();
+    pl->ntiles = pb;
+    pl->units.alloc(h_units.size());
+    pl->units.upload(h_units.data(), h_units.size(), st);
+    pl->prog.alloc(std::max(pb, 1));
   }
   pl->R = R;
   pl->code = big_code(R, U);
@@ -967,7 +999,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           GE_HIP(hipEventRecord(re[0], ss));
         }
         if (pl->sym) {
-          GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
+          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
           if (c.repel == 1.0)
             hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
                                ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,

@@ -172,8 +172,54 @@ __device__ __forceinline__ void sym_steps_any(bool fast, int s0, int s1, int lan
                                          racc, flow);
 }
 
-// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog, 0}
-// in queue order; prog zeroed before the launch; queue = one counter.
+// A row block of 64 rows against all s members in ascending order, every pair
+// evaluated for its row (the plain ordered-pair scheme: no dependencies).  Used
+// for aggregates whose sweep chain would outlast the rest of the launch.
+template <int D, bool REPEL_ONE>
+__device__ __forceinline__ void rows_block(int lane, int base, int s, int A, const double* X,
+                                           const double* DP, double repel, bool repel_ok,
+                                           double* tile, double* F) {
+  constexpr int WV = SymW<D>::v;
+  const size_t rb = (size_t)base + 64 * (size_t)A;
+  const bool rv = 64 * A + lane < s;
+  double xi[D], acc[D], di = 1.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xi[k] = rv ? X[(rb + lane) * D + k] : 0.0;
+    acc[k] = 0.0;
+  }
+  if (rv) di = DP[rb + lane];
+  const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xi, di));
+  for (int j0 = 0; j0 < s; j0 += 64) {
+    const int cnt = min(64, s - j0);
+    wave_lds_sync();  // the previous tile has been read by every lane
+    bool ok = true;
+    if (lane < cnt) {
+      const size_t c = (size_t)base + j0 + lane;
+#pragma unroll
+      for (int k = 0; k < D; ++k) tile[lane * WV + k] = X[c * D + k];
+      tile[lane * WV + D] = DP[c];
+      ok = vertex_ok<D>(&tile[lane * WV], tile[lane * WV + D]);
+    }
+    wave_lds_sync();
+    if (rows_ok && __all(ok)) {
+      for (int jj = 0; jj < cnt; ++jj)  // the j == i term is +-0 (ge_pair.hpp)
+        rep_pair<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
+    } else {
+      for (int jj = 0; jj < cnt; ++jj)
+        rep_pair<D, false, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
+    }
+  }
+  if (rv) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = acc[k];
+  }
+  wave_lds_sync();
+}
+
+// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
+// kind (0: symmetric sweep, 1: row block)} in queue order; prog zeroed before the
+// launch; queue = one counter.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3)
 template <int D, bool REPEL_ONE>
 __global__ void __launch_bounds__(kSymT, 4)
@@ -201,6 +247,10 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const int A = u.y;
     const int base = pt_ip[u.x];
     const int s = pt_ip[u.x + 1] - base;
+    if (u.w) {
+      rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
+      continue;
+    }
     int* tprog = prog + u.z + A;  // tprog[t]: column tile A + t
     const size_t cbase = (size_t)base + 64 * (size_t)A;
     const bool rv = 64 * A + lane < s;

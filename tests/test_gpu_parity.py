@@ -381,6 +381,7 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, re
     (GE_ROWS_SEGMENTS=0)."""
     monkeypatch.setenv("GE_ROWS_TILES", tiles)
     monkeypatch.setenv("GE_ROWS_SEGMENTS", segs)
+    monkeypatch.setenv("GE_FAML_SYM", "0")  # the ordered-pair kernel (faml_big_repulse)
     monkeypatch.setenv("GE_FAML_R", str(R))
     monkeypatch.setenv("GE_FAML_U", str(U))
     sizes = [3000, 700, 2203, 90, 1]
@@ -394,6 +395,31 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, re
     rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
     want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17, repel=repel)
     got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=5, seed=17, repel=repel)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("chain,dim,repel", [
+    ("0", 3, 1.0), ("0", 3, 1.5), ("0", 3, 2.0 ** 70), ("1e9", 3, 1.0), ("", 3, 1.0),
+    ("0", 2, 1.0), ("0", 4, 0.75), ("1e9", 4, 1.0)])
+def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
+    """faml_sym_repulse (ge_sym.hpp): every unordered pair once, row sums in the
+    reference's order -- all aggregates as sweeps (chain 0), all as row blocks
+    (1e9), the plan's own mix; repel = 2^70 forces the `/` path (outside the
+    shared-reciprocal domain); ragged last tiles (sizes not multiples of 64),
+    whole and one-member last tiles (320, 257), hub rows."""
+    monkeypatch.setenv("GE_FAML_SYM", "1")
+    if chain:
+        monkeypatch.setenv("GE_FAML_SYM_CHAIN", chain)
+    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]  # streamed: > 256 members
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=11), [(3, 2000), (70, 3000)], seed=dim)
+    PT = _block_partition(n, sizes, seed=5)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
     assert np.array_equal(got, want)
 
 
