@@ -14,7 +14,7 @@ mkdir -p $OUT $PROF
 export TMPDIR=/tmp
 lscpu | grep -E "Model name|^CPU\(s\)|Socket|Core\(s\)" > $OUT/host.txt
 timeout -k 10 900 python3 bench.py --workload $W --steps 20 --warmup 5 "$@" > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json; tail -4 $OUT/bench.err
+cat $OUT/bench.json; tail -4 $OUT/bench.err; cp $OUT/bench.json $PROF/bench_$W.json
 prof() {  # name, rocprof args
   local name=$1; shift
   timeout -k 10 600 rocprofv3 "$@" --output-format csv -d $OUT/$name -o $name -- \
@@ -22,8 +22,8 @@ prof() {  # name, rocprof args
   echo "$name ok"
 }
 prof trace --kernel-trace --stats &&
-prof fetch --pmc FETCH_SIZE &&
-prof write --pmc WRITE_SIZE || exit 1
+prof fetch --pmc FETCH_SIZE --kernel-include-regex "faml_|rows_kernel|heavy_|fa_repulse|fa_grouped" &&
+prof write --pmc WRITE_SIZE --kernel-include-regex "faml_|rows_kernel|heavy_|fa_repulse|fa_grouped" || exit 1
 cp $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $PROF/rocprof_kernel_stats_$W.csv
 cp $(find $OUT/fetch -name "*counter_collection.csv" | head -1) $PROF/pmc_fetch_$W.csv
 cp $(find $OUT/write -name "*counter_collection.csv" | head -1) $PROF/pmc_write_$W.csv
