@@ -89,6 +89,12 @@ def host_info():
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except AttributeError:
         pass
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpuset.cpus.effective"):
+        try:
+            with open(path) as f:
+                info[os.path.basename(path)] = f.read().strip()
+        except OSError:
+            pass
     try:
         import subprocess
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -120,19 +126,23 @@ def baseline_threads():
 
 def baseline_record(value, unit, threads, sample, per_iter):
     hi = host_info()
-    rec = {"value": value, "unit": unit, "cores": threads, "kind": "port", "sample": sample,
+    # the threads that can run at once: the OpenMP threads, bounded by the CPUs this
+    # process may use (the GPU box confines a job to a small CPU share)
+    cores = min(threads, hi.get("affinity_cpus") or threads)
+    rec = {"value": value, "unit": unit, "cores": cores, "omp_threads": threads, "kind": "port",
+           "sample": sample,
            "seconds_per_iteration": per_iter, "host": hi,
            "omp": {"OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
                    "OMP_PROC_BIND": os.environ.get("OMP_PROC_BIND"),
                    "OMP_PLACES": os.environ.get("OMP_PLACES")}}
     pc = hi.get("physical_cores")
-    if pc and pc > threads:
+    if pc and pc > cores:
         # the reference's loops are `omp parallel for` over independent rows /
         # aggregates: perfect scaling to every physical core bounds what the whole
         # host could do (an extrapolation, not a measurement)
-        rec["extrapolated_all_physical_cores"] = {"value": value * pc / threads, "cores": pc,
+        rec["extrapolated_all_physical_cores"] = {"value": value * pc / cores, "cores": pc,
                                                   "note": "linear scaling from the measured "
-                                                          "threads; upper bound"}
+                                                          "cores; upper bound, not measured"}
     return rec
 
 
@@ -320,7 +330,8 @@ def run_multilevel(args, rank, world, local, dev):
     elapsed = timed(args, world, dev, steps)
     rep_ms, rep_launches, rep_pairs = pk.repulse_ms()
     res_ms, str_ms, _ = pk.kernel_ms()
-    traffic, traffic_src = pmc_traffic_per_launch("faml_big_repulse", args.workload)
+    rep_kernel = "faml_big_repulse" if os.environ.get("GE_FAML_SYM") == "0" else "faml_sym_repulse"
+    traffic, traffic_src = pmc_traffic_per_launch(rep_kernel, args.workload)
     finite = bool(torch.isfinite(X).all().item())
     sizes = np.diff(PT[0]).astype(np.float64)
     pairs = float((sizes * (sizes - 1)).sum())
@@ -344,14 +355,16 @@ def run_multilevel(args, rank, world, local, dev):
         "edges_per_s": nnz0 * its,
         "pair_interactions_per_s": pairs * its,
         "finite": finite,
-        "roofline": {"kernel": "faml_big_repulse (streamed in-aggregate all-pairs repulsion, "
-                               "strict fp64)",
+        "roofline": {"kernel": f"{rep_kernel} (streamed in-aggregate all-pairs repulsion, "
+                               "strict fp64; one launch per iteration)",
                      "bound": "valu", "pipe": "fp64 VALU; priced against the FP64 vector peak "
                                               "(78.6 TFLOP/s, spec)",
                      "achieved": rep_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": rep_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "flops_per_launch": rep_flops,
-                     "flops_per_unit": "26 per ordered in-aggregate pair (7d+5, d=3)",
+                     "flops_per_unit": "26 per ordered in-aggregate pair (7d+5, d=3); the "
+                                       "symmetric kernel evaluates each unordered pair once "
+                                       "and credits both ordered pairs",
                      "avg_launch_ms": rep_ms, "launches": rep_launches},
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
         "setup_seconds": {"graph_host": t_gen, "partition_device": t_part,

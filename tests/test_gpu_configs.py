@@ -52,9 +52,11 @@ def test_c2_full_size_iteration_sampled_rows(ctx, oracle):
     deg = oracle.degrees(A)
     rows = _rows_sample(n, np.diff(A[0]), np.random.default_rng(1))
     want = X0.copy()
-    for r in rows:  # one row per call: the oracle's fa_step_rows works on [rb, re)
+    # one row per call (the oracle's fa_step_rows works on [rb, re)); no thread-count
+    # override: omp_set_num_threads would also bind libge's later OpenMP regions
+    for r in rows:
         fprev = np.zeros((1, 3))
-        oracle.fa_step_rows(A, X0, deg, int(r), int(r) + 1, fprev, want, nthreads=1)
+        oracle.fa_step_rows(A, X0, deg, int(r), int(r) + 1, fprev, want)
     assert np.array_equal(got[rows], want[rows])
     assert np.isfinite(got).all()
 
@@ -116,8 +118,7 @@ def test_c5_attraction_pass_sampled_rows(oracle):
     want = X.copy()
     for r, fr in zip(rows, frep_rows):
         fprev = np.zeros((1, 3))
-        oracle.fa_step_rows_frep(A, X, deg, int(r), int(r) + 1, fr[None, :], fprev, want,
-                                 nthreads=1)
+        oracle.fa_step_rows_frep(A, X, deg, int(r), int(r) + 1, fr[None, :], fprev, want)
     _progress(t0, "C5 oracle rows done")
     assert np.array_equal(got, want[rows])
 
