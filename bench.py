@@ -256,12 +256,26 @@ def timed(args, world, dev, fn):
     return elapsed
 
 
+def make_comm(ctx, rank, world):
+    """The library's communicator (ge_comm): RCCL inside libge, its unique id
+    broadcast from rank 0 over the harness's process group; GE_DIST_BACKEND=gloo
+    (several ranks sharing one GPU) uses the library's host transport instead."""
+    import torch.distributed as dist
+    import ge_amd as ge
+    if world == 1:
+        return None
+    if dist.get_backend() != "nccl":
+        return ge.Comm(ctx, world, rank, backend="transport")
+    box = [ge.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return ge.Comm(ctx, world, rank, backend="rccl", uid=box[0])
+
+
 def run_multilevel(args, rank, world, local, dev):
     """configs[2] / configs[3]: R-MAT -> LCC -> device partition(A, 0.125), first 4 P_T
     -> device P^T A P -> K forceAtlasMultilevel iterations of level 0."""
     import torch
     import ge_amd as ge
-    from ge_amd.dist import aggregate_cost, assign_aggregates, member_rows, allgather_members
     t0 = time.perf_counter()
     L = ge.largest_component(ge.rmat_csr(args.n, args.draws, seed=args.seed))
     t_gen = time.perf_counter() - t0
@@ -301,9 +315,16 @@ def run_multilevel(args, rank, world, local, dev):
     torch.cuda.set_stream(work)
     ctx.set_stream(work.cuda_stream)
     torch.cuda.synchronize(dev)
-    owned, loads = assign_aggregates(aggregate_cost(PT[0], L[0], PT[1]), world)
-    rows = [member_rows(PT[0], PT[1], o) for o in owned]
-    log(rank, f"aggregate shards: loads {[f'{x:.3g}' for x in loads]}")
+    comm = make_comm(ctx, rank, world)
+    # aggregates dealt to ranks by cost inside libge (ge_assign_aggregates: LPT on
+    # s(s-1) + the members' CSR entries)
+    owner = ge.assign_aggregates(PT, L[0], world)
+    mine = np.flatnonzero(owner == rank).astype(np.int32)
+    if world > 1:
+        from ge_amd.dist import aggregate_cost
+        cost = aggregate_cost(PT[0], L[0], PT[1])
+        log(rank, f"aggregate shards: loads "
+                  f"{[f'{cost[owner == r].sum():.3g}' for r in range(world)]}")
     plans = {}
 
     def plan_for(iters):
@@ -311,7 +332,7 @@ def run_multilevel(args, rank, world, local, dev):
             plans[iters] = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(),
                                        d["dx"].data_ptr(), PT[0], d["pip"].data_ptr(),
                                        d["pix"].data_ptr(), d["vA"].data_ptr(), args.dim,
-                                       iterations=iters, aggs=owned[rank] if world > 1 else None)
+                                       iterations=iters, aggs=mine if world > 1 else None)
         return plans[iters]
 
     pk = plan_for(args.steps)
@@ -325,7 +346,8 @@ def run_multilevel(args, rank, world, local, dev):
         if timed:
             p.set_profiling(True)
         p.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
-        allgather_members(X, rows, rank, world)
+        if comm is not None:  # one all-gather of the members' coordinates (libge, RCCL)
+            comm.allgather_members(X.data_ptr(), args.dim, PT, owner)
 
     elapsed = timed(args, world, dev, steps)
     rep_ms, rep_launches, rep_pairs = pk.repulse_ms()
@@ -351,7 +373,10 @@ def run_multilevel(args, rank, world, local, dev):
                                "aggregate, strict fp64",
                    "n": n0, "nnz": nnz0, "aggregates": m, "dim": args.dim,
                    "levels": [h[2] for h in hier],
-                   "parallelism": f"aggregates{world}" + ("+member-allgather" if world > 1 else "")},
+                   "parallelism": f"aggregates{world}" + ("+member-allgather(libge " +
+                                                          ("rccl" if comm.info()[2] else
+                                                           "transport") + ")"
+                                                          if world > 1 else "")},
         "edges_per_s": nnz0 * its,
         "pair_interactions_per_s": pairs * its,
         "finite": finite,
@@ -372,6 +397,8 @@ def run_multilevel(args, rank, world, local, dev):
     }
     for p in plans.values():
         p.close()
+    if comm is not None:
+        comm.close()
     if rank == 0 and world == 1 and not args.no_end_to_end:
         t0 = time.perf_counter()
         Xe = ctx.embed(As, hier, args.dim, seed=args.seed)
@@ -392,14 +419,15 @@ def run_single_level(args, rank, world, local, dev):
     """configs[1]: single-level forceAtlas, one step = one iteration."""
     import torch
     import ge_amd as ge
-    from ge_amd.dist import ShardedForceAtlas
+    from ge_amd.dist import row_shards
     t0 = time.perf_counter()
     A = ge.rmat_csr(args.n, args.draws, seed=args.seed)
     n, nnz = len(A[0]) - 1, len(A[1])
     X0 = ge.uniform_stream(args.seed, n * args.dim).reshape(n, args.dim)  # ref init order
     log(rank, f"R-MAT n={n} nnz={nnz} generated in {time.perf_counter() - t0:.1f}s")
-    drv = ShardedForceAtlas(n, world, rank, None)
-    npad, rb, re = drv.padded_rows, drv.rb, drv.re
+    chunk, shards = row_shards(n, world)
+    npad = chunk * world
+    rb, re = shards[rank]
     ip, ix, dx = (torch.from_numpy(a).to(dev) for a in A)
     xa = torch.zeros((npad, args.dim), dtype=torch.float64, device=dev)
     xa[:n] = torch.from_numpy(X0).to(dev)
@@ -409,17 +437,19 @@ def run_single_level(args, rank, world, local, dev):
     torch.cuda.set_stream(work)
     ctx.set_stream(work.cuda_stream)
     torch.cuda.synchronize(dev)
+    comm = make_comm(ctx, rank, world)
     mode = ge.MODE_FAST if args.mode == "fast" else ge.MODE_STRICT
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), args.dim, rb, re,
                        mode=mode)
-    drv.step_rows = lambda cur, nxt, rb_, re_: plan.step(cur.data_ptr(), nxt.data_ptr())
     buf = [xa, xb]
 
     def steps(k, timed):
         if timed:
             plan.set_profiling(True)
         for _ in range(k):
-            drv.step(buf[0], buf[1])
+            plan.step(buf[0].data_ptr(), buf[1].data_ptr())
+            if comm is not None:  # one in-place all-gather of the rows (libge, RCCL)
+                comm.allgather_coords(buf[1].data_ptr(), chunk, args.dim)
             buf.reverse()
 
     elapsed = timed(args, world, dev, steps)
@@ -465,6 +495,8 @@ def run_single_level(args, rank, world, local, dev):
         result["cpu_baseline"] = cpu_baseline_fa(A, X0, args.cpu_baseline_seconds, rank)
         result["vs_cpu_baseline"] = its / result["cpu_baseline"]["value"]
     plan.close()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

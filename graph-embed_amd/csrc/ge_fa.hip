@@ -198,7 +198,9 @@ fa_repulse_strict(int n, int rb, int re, int per_block, const double* __restrict
           const double dj = tile[jj * W + D];
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (r < nr) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+            if (r < nr)
+              rep_pair_fb<D, REPEL_ONE>(xi[r], xj, di[r], dj, repel,
+                                        j0 + jj == c0 + tid + r * kRepThreads, acc[r]);
         }
       }
     }
@@ -596,8 +598,6 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
       // :151-167, j ascending; then :169-203, CSR order
       pipelined_group_sum<D, G, T>(n, tid, g, tb, [&](int q, double (&t)[D]) {
         const int jj = min(q, n - 1);
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = 0.0;
         rep_term<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t);
         if (q >= n)
 #pragma unroll
@@ -621,8 +621,6 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
         for (int u = 0; u < U; ++u) {
           const int j = j0 + g + G * u;
           const int jj = min(j, n - 1);
-#pragma unroll
-          for (int k = 0; k < D; ++k) t[u][k] = 0.0;
           rep_term<D, true, false>(xi, &sx[jj * W], dip1, sx[jj * W + D], c.repel, t[u]);
           if (j >= n)
 #pragma unroll
@@ -659,7 +657,7 @@ fa_small_strict(int n, const int* __restrict__ ip, const int* __restrict__ ixg,
             if (rep_ok && vertex_ok<D>(xj, sx[j * W + D]))
               rep_pair<D, true, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
             else
-              rep_pair<D, false, false>(xi, xj, dip1, sx[j * W + D], c.repel, t[u]);
+              rep_pair_fb<D, false>(xi, xj, dip1, sx[j * W + D], c.repel, j == i, t[u]);
           }
         }
         group_add<D, G, U>(t, tid, g, min(G * U, n - j0), leader, tb, acc);
@@ -851,8 +849,6 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
     if (G > 1) {
       pipelined_group_sum<D, G, kGrpT>(n, tid, g, tb, [&](int q, double (&t)[D]) {
         const int jj = min(q, n - 1);
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = 0.0;
         rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], repel, t);
         if (q >= n)
 #pragma unroll
@@ -874,7 +870,7 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
         if (row_ok && vertex_ok<D>(xj, rec[j * W + D]))
           rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], repel, t[0]);
         else
-          rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], repel, t[0]);
+          rep_pair_fb<D, REPEL_ONE>(xi, xj, di, rec[j * W + D], repel, j == i, t[0]);
       }
       group_add<D, G, 1>(t, tid, g, min(G, n - j0), active && g == 0, tb, acc);
     }
@@ -924,8 +920,6 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
   if (__syncthreads_and(ok) && G > 1) {  // block-uniform: every record in the domain
     pipelined_group_sum<D, G, kGrpT>(n, tid, g, tb, [&](int q, double (&t)[D]) {
       const int jj = min(q, n - 1);
-#pragma unroll
-      for (int k = 0; k < D; ++k) t[k] = 0.0;
       rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
       if (q >= n)
 #pragma unroll
@@ -954,7 +948,7 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
         if (row_ok && vertex_ok<D>(xj, rec[j * W + D]))
           rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
         else
-          rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+          rep_pair_fb<D, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, j == i, t[0]);
       }
       group_add<D, G, 1>(t, tid, g, min(G, n - j0), active && g == 0, tb, acc);
     }
@@ -1026,8 +1020,6 @@ fa_grouped_stream(int n, int rb, int re, const int* __restrict__ ip, const int* 
     if (__syncthreads_and(ok) && G > 1) {  // block-uniform: row and tile in the domain
       pipelined_group_sum<D, G, kGrpT>(cnt, tid, g, tb, [&](int q, double (&t)[D]) {
         const int jj = min(q, cnt - 1);
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = 0.0;
         rep_term<D, true, REPEL_ONE>(xi, &rec[jj * W], di, rec[jj * W + D], c.repel, t);
         if (q >= cnt)
 #pragma unroll
@@ -1045,7 +1037,7 @@ fa_grouped_stream(int n, int rb, int re, const int* __restrict__ ip, const int* 
           if (rok && vertex_ok<D>(xj, rec[j * W + D]))
             rep_pair<D, true, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
           else
-            rep_pair<D, false, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t[0]);
+            rep_pair_fb<D, REPEL_ONE>(xi, xj, di, rec[j * W + D], c.repel, t0 + j == i, t[0]);
         }
         group_add<D, G, 1>(t, tid, g, min(G, cnt - j0), active && g == 0, tb, acc);
       }

@@ -106,7 +106,7 @@ __device__ __forceinline__ void member_force(int li, int s, int a, int v, const 
     if (rep_ok && vertex_ok<D>(xj, ds(j)))
       rep_pair<D, true, false>(xi, xj, dip1, ds(j), c.repel, acc);
     else
-      rep_pair<D, false, false>(xi, xj, dip1, ds(j), c.repel, acc);
+      rep_pair_fb<D, false>(xi, xj, dip1, ds(j), c.repel, j == li, acc);
   }
   double m2 = xi[0] * xi[0];
 #pragma unroll
@@ -453,7 +453,9 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
           const double dj = tile[jj * WV + D];
 #pragma unroll
           for (int r = 0; r < R; ++r)
-            if (r < nr) rep_pair<D, false, REPEL_ONE>(xi[r], xj, di[r], dj, repel, acc[r]);
+            if (r < nr)
+              rep_pair_fb<D, REPEL_ONE>(xi[r], xj, di[r], dj, repel,
+                                        j0 + jj == r0 + lane + 64 * r, acc[r]);
         }
       }
     }

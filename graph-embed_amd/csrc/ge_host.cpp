@@ -60,20 +60,6 @@ inline double norm_of(const double* v, int dim) {
   return std::sqrt(acc);
 }
 
-// Device copy of a host CSR.
-struct DevCsr {
-  DevBuf<int> ip, ix;
-  DevBuf<double> dx;
-  int n = 0, nnz = 0;
-  DevCsr(int rows, const int* hip_, const int* hix, const double* hdx, hipStream_t s)
-      : ip(rows + 1), ix(std::max(hip_[rows], 1)), dx(std::max(hip_[rows], 1)), n(rows),
-        nnz(hip_[rows]) {
-    ip.upload(hip_, rows + 1, s);
-    ix.upload(hix, nnz, s);
-    dx.upload(hdx, nnz, s);
-  }
-};
-
 // ---------------------------------------------------------------------------
 // radius step (src/embed.cpp:615-777)
 
@@ -194,6 +180,8 @@ void radius_step(int m, double* cA, double* rA, int dim, bool base, int mc, cons
   }
 }
 
+}  // namespace
+
 // ---------------------------------------------------------------------------
 // multilevel FA on the device from host arrays
 
@@ -219,6 +207,23 @@ void faml_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* d
   GE_HIP(hipStreamSynchronize(s));
 }
 
+// normalize (include/forceatlas.hpp:272-303), serial as the reference
+void normalize_host(double* X, int n, int dim) {
+  std::vector<double> avg(dim, 0.0);
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < dim; ++k) avg[k] = avg[k] + X[(size_t)i * dim + k];
+  for (int k = 0; k < dim; ++k) avg[k] = avg[k] / n;
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < dim; ++k) X[(size_t)i * dim + k] -= avg[k];
+  double longest = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double len = norm_of(X + (size_t)i * dim, dim);
+    if (longest < len) longest = len;
+  }
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < dim; ++k) X[(size_t)i * dim + k] = X[(size_t)i * dim + k] / longest;
+}
+
 void fa_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx, int dim,
              double* X, bool init_random, int iterations, const ge_fa_params& p) {
   if (init_random) uniform_stream(p.seed, (size_t)n * dim, X);  // :118-125
@@ -230,22 +235,84 @@ void fa_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx,
   fa_run_device(ctx, n, A.nnz, A.ip.p, A.ix.p, A.dx.p, dim, dX.p, iterations, p);
   dX.download(X, (size_t)n * dim, s);
   GE_HIP(hipStreamSynchronize(s));
-  if (p.normalize) {  // :272-303, serial as the reference
-    std::vector<double> avg(dim, 0.0);
-    for (int i = 0; i < n; ++i)
-      for (int k = 0; k < dim; ++k) avg[k] = avg[k] + X[(size_t)i * dim + k];
-    for (int k = 0; k < dim; ++k) avg[k] = avg[k] / n;
-    for (int i = 0; i < n; ++i)
-      for (int k = 0; k < dim; ++k) X[(size_t)i * dim + k] -= avg[k];
-    double longest = 0.0;
-    for (int i = 0; i < n; ++i) {
-      double len = norm_of(X + (size_t)i * dim, dim);
-      if (longest < len) longest = len;
-    }
-    for (int i = 0; i < n; ++i)
-      for (int k = 0; k < dim; ++k) X[(size_t)i * dim + k] = X[(size_t)i * dim + k] / longest;
-  }
+  if (p.normalize) normalize_host(X, n, dim);
 }
+
+// ---------------------------------------------------------------------------
+// embed orchestration (src/embed.cpp:561-796): the coarsest level's forceAtlas
+// (:586), then per finer level the radius step (:615-777) and
+// forceAtlasMultilevel (:793).  With a communicator of more than one rank the
+// level calls run sharded (ge_dist.hip); the host radius step is replicated.
+
+void embed_impl(ge_ctx* ctx, ge_comm* comm, int levels, const int* a_n, const int* a_off,
+                const int* a_nz_off, const int* a_ip, const int* a_ix, const double* a_dx,
+                const int* p_rows, const int* p_off, const int* p_nz_off, const int* p_ip,
+                const int* p_ix, int dim, int base_iterations, int ml_iterations,
+                int print_progress, const ge_fa_params& p, double* coords_out) {
+  const bool dist = comm && comm->nranks > 1;
+  auto fa_level = [&](int n, const int* ip, const int* ix, const double* dx, int d, double* X,
+                      bool init, int it, const ge_fa_params& pr) {
+    if (dist) fa_host_dist(comm, n, ip, ix, dx, d, X, init, it, pr);
+    else fa_host(ctx, n, ip, ix, dx, d, X, init, it, pr);
+  };
+  auto faml_level = [&](int n, const int* ip, const int* ix, const double* dx, int m,
+                        const int* pip, const int* pix, const int* vA, const double* cA,
+                        const double* rA, double* X, int d, int it, const ge_fa_params& pr) {
+    if (dist) faml_host_dist(comm, n, ip, ix, dx, m, pip, pix, vA, cA, rA, X, d, it, pr);
+    else faml_host(ctx, n, ip, ix, dx, m, pip, pix, vA, cA, rA, X, d, it, pr);
+  };
+  GE_REQUIRE(coords_out && a_n && a_off && a_nz_off, "null argument");
+  GE_REQUIRE(levels >= 0 && dim >= 1 && dim <= 4, "bad levels or dimension");
+  for (int l = 0; l < levels; ++l)  // src/embed.cpp:564-570
+    GE_REQUIRE(p_rows[l] == a_n[l + 1], "As[l+1].Rows() must equal P_Ts[l].Rows()");
+  auto Aip = [&](int l) { return a_ip + a_off[l]; };
+  auto Aix = [&](int l) { return a_ix + a_nz_off[l]; };
+  auto Adx = [&](int l) { return a_dx + a_nz_off[l]; };
+  auto Pip = [&](int l) { return p_ip + p_off[l]; };
+  auto Pix = [&](int l) { return p_ix + p_nz_off[l]; };
+  for (int l = 0; l < levels; ++l)
+    GE_REQUIRE(Pip(l)[p_rows[l]] == a_n[l], "As[l].Rows() must equal P_Ts[l].Cols()");
+
+  const int L = levels;
+  const bool prof = std::getenv("GE_PROFILE_EMBED") != nullptr;
+  auto clk = [] { return std::chrono::steady_clock::now(); };
+  auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
+  if (print_progress) std::cout << "embedding layer " << L + 1 << ": getting base coords" << std::endl;
+  std::vector<double> coarse((size_t)a_n[L] * dim);
+  auto t0 = clk();
+  fa_level(a_n[L], Aip(L), Aix(L), Adx(L), dim, coarse.data(), true, base_iterations, p);
+  if (prof)
+    std::fprintf(stderr, "embed: coarsest forceAtlas n=%d %d iterations %.3fs\n", a_n[L],
+                 base_iterations, secs(t0, clk()));
+  std::vector<double> r_coarse, cAc;
+  for (int l = L - 1; l >= 0; --l) {
+    if (print_progress) std::cout << "embeding layer " << l + 1 << std::endl;  // sic (:613)
+    const int m = a_n[l + 1];
+    const bool base = (l + 1 == L);
+    std::vector<double> rA(m);
+    auto t1 = clk();
+    radius_step(m, coarse.data(), rA.data(), dim, base, base ? 0 : p_rows[l + 1],
+                base ? nullptr : Pip(l + 1), base ? nullptr : Pix(l + 1),
+                base ? nullptr : cAc.data(), base ? nullptr : r_coarse.data(), Aip(l + 1),
+                Aix(l + 1));
+    auto t2 = clk();
+    std::vector<int> vA(a_n[l]);
+    for (int a = 0; a < m; ++a)
+      for (int c = Pip(l)[a]; c < Pip(l)[a + 1]; ++c) vA[Pix(l)[c]] = a;
+    std::vector<double> fine((size_t)a_n[l] * dim, 0.0);
+    faml_level(a_n[l], Aip(l), Aix(l), Adx(l), m, Pip(l), Pix(l), vA.data(), coarse.data(),
+               rA.data(), fine.data(), dim, ml_iterations, p);
+    if (prof)
+      std::fprintf(stderr, "embed: level %d n=%d: radius step %.3fs, forceAtlasMultilevel %.3fs\n",
+                   l, a_n[l], secs(t1, t2), secs(t2, clk()));
+    cAc = std::move(coarse);
+    r_coarse = std::move(rA);
+    coarse = std::move(fine);
+  }
+  std::memcpy(coords_out, coarse.data(), sizeof(double) * coarse.size());
+}
+
+namespace {
 
 // ---------------------------------------------------------------------------
 // synthetic R-MAT + LCC (definition: tests/graphs.py)
@@ -476,7 +543,7 @@ int ge_ptap(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx, 
       ge::DevBuf<int> dpip(m + 1), dpix(std::max(n, 1));
       dpip.upload(pip, m + 1, s);
       dpix.upload(pix, n, s);
-      ge::ptap_device(ctx, n, A.ip.p, A.ix.p, A.dx.p, A.nnz, m, dpip.p, dpix.p, c);
+      ge::ptap_device(ctx, n, A.ip.p, A.ix.p, A.dx.p, A.nnz, m, pip, dpip.p, dpix.p, 0, m, c);
     } catch (...) {
       delete c;
       throw;
@@ -538,57 +605,25 @@ int ge_embed(ge_ctx* ctx, int levels, const int* a_n, const int* a_off, const in
              int base_iterations, int ml_iterations, int print_progress, const ge_fa_params* pp,
              double* coords_out) {
   return guarded([&] {
-    GE_REQUIRE(ctx && pp && coords_out && a_n && a_off && a_nz_off, "null argument");
-    GE_REQUIRE(levels >= 0 && dim >= 1 && dim <= 4, "bad levels or dimension");
-    for (int l = 0; l < levels; ++l)  // src/embed.cpp:564-570
-      GE_REQUIRE(p_rows[l] == a_n[l + 1], "As[l+1].Rows() must equal P_Ts[l].Rows()");
+    GE_REQUIRE(ctx && pp, "null argument");
     ge::DeviceGuard g(ctx);
-    const ge_fa_params p = *pp;
-    auto Aip = [&](int l) { return a_ip + a_off[l]; };
-    auto Aix = [&](int l) { return a_ix + a_nz_off[l]; };
-    auto Adx = [&](int l) { return a_dx + a_nz_off[l]; };
-    auto Pip = [&](int l) { return p_ip + p_off[l]; };
-    auto Pix = [&](int l) { return p_ix + p_nz_off[l]; };
-    for (int l = 0; l < levels; ++l)
-      GE_REQUIRE(Pip(l)[p_rows[l]] == a_n[l], "As[l].Rows() must equal P_Ts[l].Cols()");
+    ge::embed_impl(ctx, nullptr, levels, a_n, a_off, a_nz_off, a_ip, a_ix, a_dx, p_rows, p_off,
+                   p_nz_off, p_ip, p_ix, dim, base_iterations, ml_iterations, print_progress, *pp,
+                   coords_out);
+  });
+}
 
-    const int L = levels;
-    const bool prof = std::getenv("GE_PROFILE_EMBED") != nullptr;
-    auto clk = [] { return std::chrono::steady_clock::now(); };
-    auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
-    if (print_progress) std::cout << "embedding layer " << L + 1 << ": getting base coords" << std::endl;
-    std::vector<double> coarse((size_t)a_n[L] * dim);
-    auto t0 = clk();
-    ge::fa_host(ctx, a_n[L], Aip(L), Aix(L), Adx(L), dim, coarse.data(), true, base_iterations, p);
-    if (prof)
-      std::fprintf(stderr, "embed: coarsest forceAtlas n=%d %d iterations %.3fs\n", a_n[L],
-                   base_iterations, secs(t0, clk()));
-    std::vector<double> r_coarse, cAc;
-    for (int l = L - 1; l >= 0; --l) {
-      if (print_progress) std::cout << "embeding layer " << l + 1 << std::endl;  // sic (:613)
-      const int m = a_n[l + 1];
-      const bool base = (l + 1 == L);
-      std::vector<double> rA(m);
-      auto t1 = clk();
-      ge::radius_step(m, coarse.data(), rA.data(), dim, base, base ? 0 : p_rows[l + 1],
-                      base ? nullptr : Pip(l + 1), base ? nullptr : Pix(l + 1),
-                      base ? nullptr : cAc.data(), base ? nullptr : r_coarse.data(), Aip(l + 1),
-                      Aix(l + 1));
-      auto t2 = clk();
-      std::vector<int> vA(a_n[l]);
-      for (int a = 0; a < m; ++a)
-        for (int c = Pip(l)[a]; c < Pip(l)[a + 1]; ++c) vA[Pix(l)[c]] = a;
-      std::vector<double> fine((size_t)a_n[l] * dim, 0.0);
-      ge::faml_host(ctx, a_n[l], Aip(l), Aix(l), Adx(l), m, Pip(l), Pix(l), vA.data(),
-                    coarse.data(), rA.data(), fine.data(), dim, ml_iterations, p);
-      if (prof)
-        std::fprintf(stderr, "embed: level %d n=%d: radius step %.3fs, forceAtlasMultilevel %.3fs\n",
-                     l, a_n[l], secs(t1, t2), secs(t2, clk()));
-      cAc = std::move(coarse);
-      r_coarse = std::move(rA);
-      coarse = std::move(fine);
-    }
-    std::memcpy(coords_out, coarse.data(), sizeof(double) * coarse.size());
+int ge_embed_dist(ge_comm* comm, int levels, const int* a_n, const int* a_off,
+                  const int* a_nz_off, const int* a_ip, const int* a_ix, const double* a_dx,
+                  const int* p_rows, const int* p_off, const int* p_nz_off, const int* p_ip,
+                  const int* p_ix, int dim, int base_iterations, int ml_iterations,
+                  int print_progress, const ge_fa_params* pp, double* coords_out) {
+  return guarded([&] {
+    GE_REQUIRE(comm && comm->ctx && pp, "null argument");
+    ge::DeviceGuard g(comm->ctx);
+    ge::embed_impl(comm->ctx, comm, levels, a_n, a_off, a_nz_off, a_ip, a_ix, a_dx, p_rows, p_off,
+                   p_nz_off, p_ip, p_ix, dim, base_iterations, ml_iterations,
+                   print_progress && comm->rank == 0, *pp, coords_out);
   });
 }
 

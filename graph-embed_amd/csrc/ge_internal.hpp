@@ -85,12 +85,35 @@ struct DevBuf {
   }
 };
 
+// Device copy of a host CSR.
+struct DevCsr {
+  DevBuf<int> ip, ix;
+  DevBuf<double> dx;
+  int n = 0, nnz = 0;
+  DevCsr(int rows, const int* hip_, const int* hix, const double* hdx, hipStream_t s)
+      : ip(rows + 1), ix(hip_[rows] > 0 ? hip_[rows] : 1), dx(hip_[rows] > 0 ? hip_[rows] : 1),
+        n(rows), nnz(hip_[rows]) {
+    ip.upload(hip_, rows + 1, s);
+    ix.upload(hix, nnz, s);
+    dx.upload(hdx, nnz, s);
+  }
+};
+
 }  // namespace ge
 
 struct ge_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+};
+
+// A communicator (ge_dist.hip): RCCL, or a caller transport staged through host
+// memory.  `nccl` is an ncclComm_t kept opaque here.
+struct ge_comm {
+  ge_ctx* ctx = nullptr;
+  int nranks = 1, rank = 0;
+  void* nccl = nullptr;
+  ge_transport tp{};
 };
 
 // Host CSR (returned to callers through ge_csr*).
@@ -138,7 +161,30 @@ ge_hier* partition_incremental(int n, const int* I, const int* J, const double* 
 // (non-integer weights, asymmetric A, rows not strictly ascending).
 ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const double* Dv,
                           double cf, bool printing, bool positive, double stall, int matching);
+// Coarse rows [a0, a1) of P_T A P_T^T (a0 = 0, a1 = m: the whole matrix) into a
+// host CSR of a1 - a0 rows and m columns.  h_pt_ip: P_T's indptr on the host.
 void ptap_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
-                 int nnz, int m, const int* d_pt_ip, const int* d_pt_ix, ge_csr* out);
+                 int nnz, int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
+                 int a0, int a1, ge_csr* out);
+
+// Host-array drivers (ge_host.cpp) and their sharded forms (ge_dist.hip).
+void fa_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx, int dim,
+             double* X, bool init_random, int iterations, const ge_fa_params& p);
+void faml_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* dx, int m,
+               const int* pip, const int* pix, const int* vA, const double* cA,
+               const double* rA, double* X, int dim, int iterations, const ge_fa_params& p);
+void normalize_host(double* X, int n, int dim);
+void fa_host_dist(ge_comm* comm, int n, const int* ip, const int* ix, const double* dx, int dim,
+                  double* X, bool init_random, int iterations, const ge_fa_params& p);
+void faml_host_dist(ge_comm* comm, int n, const int* ip, const int* ix, const double* dx, int m,
+                    const int* pip, const int* pix, const int* vA, const double* cA,
+                    const double* rA, double* X, int dim, int iterations,
+                    const ge_fa_params& p);
+// the embed orchestration (src/embed.cpp:561-796); comm == nullptr: one GPU
+void embed_impl(ge_ctx* ctx, ge_comm* comm, int levels, const int* a_n, const int* a_off,
+                const int* a_nz_off, const int* a_ip, const int* a_ix, const double* a_dx,
+                const int* p_rows, const int* p_off, const int* p_nz_off, const int* p_ip,
+                const int* p_ix, int dim, int base_iterations, int ml_iterations,
+                int print_progress, const ge_fa_params& p, double* coords_out);
 
 }  // namespace ge

@@ -93,7 +93,9 @@ __device__ __forceinline__ void rep_term(const double (&xi)[D], const double* __
   }
 }
 
-// rep_term added to acc.
+// rep_term added to acc.  Every sum that receives terms starts from a +0.0
+// accumulator and is never seeded with a term: a term may be -0 (e_k = -0), and
+// only the +0 start makes adding it an identity (RN: +0 + -0 = +0).
 template <int D, bool SHARED, bool REPEL_ONE>
 __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __restrict__ xj,
                                          double dip1, double djp1, double repel,
@@ -102,6 +104,17 @@ __device__ __forceinline__ void rep_pair(const double (&xi)[D], const double* __
   rep_term<D, SHARED, REPEL_ONE>(xi, xj, dip1, djp1, repel, t);
 #pragma unroll
   for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[k];
+}
+
+// The out-of-domain (`/`) form with the self pair skipped as the reference does
+// (j != i, :151).  In the shared-reciprocal domain the self term is +-0 and may
+// be accumulated, but outside it cij / eps^2 can overflow (cij > ~1.8e298) and
+// 0 * inf would put a NaN into the row's sum.
+template <int D, bool REPEL_ONE>
+__device__ __forceinline__ void rep_pair_fb(const double (&xi)[D], const double* __restrict__ xj,
+                                            double dip1, double djp1, double repel, bool self,
+                                            double (&acc)[D]) {
+  if (!self) rep_pair<D, false, REPEL_ONE>(xi, xj, dip1, djp1, repel, acc);
 }
 
 // attraction_mag for linlog == 0 and delta == 1 (the defaults): no log / pow

@@ -4,21 +4,36 @@
 // examples/embed.cpp:96-98 and examples/embedder.cpp:213-216 (linalgcpp, not
 // vendored).  A_c[a][b] = sum of A[i][j] over i in aggregate a, j in b.
 //
-// Aggregation SpGEMM by sort + run-length reduce (no GEMM shape: integer keys
-// and a stream of fp64 weights, HBM-bound):
-//   1. expand: for every P_T position c (aggregate a = row of c, member
-//      i = pt_ix[c]) and every CSR entry (i, j, w): key1 = (a << 32) | j, val w.
-//      Entries are emitted in (c, CSR) order.
-//   2. stable radix sort by key1; sum each run in emission order  -> B = P_T A
-//   3. key2 = (a << 32) | agg(j) for every B entry; stable sort; sum each run in
-//      ascending-j order -> C = B P, rows and columns ascending.
-// Pinned summation order (identical to oracle/ge_oracle.cpp orc_ptap): B[a][j]
-// adds members in P_T row order, C[a][b] adds B's columns ascending.  For the
-// unit weights of every benchmark graph all sums are exact integers.
+// Pinned summation order (identical to oracle/ge_oracle.cpp orc_ptap): B = P_T A
+// adds, for each (a, j), the members of a in P_T row order; C = B P adds, for
+// each (a, b), B's columns j ascending.  For the unit weights of every benchmark
+// graph all sums are exact integers, so the pin matters only for fractional
+// weights.
+//
+// Aggregation SpGEMM by sort + segmented serial sums (integer keys and a stream
+// of fp64 weights; HBM-bound, no GEMM shape):
+//   1. expand: one thread per emitted entry (P_T position c, CSR entry (i, j, w)
+//      of member i = pt_ix[c]), entries numbered in (c, CSR) order; a thread
+//      finds its position by binary search over the row-length prefix sums, so
+//      a hub row's entries spread over many lanes and every store coalesces.
+//   2. one stable radix sort by the composite key (a, b = agg(j), j): equal keys
+//      keep emission (= P_T member) order.  When the three fields need more than
+//      64 bits (graphs beyond ~2^21 vertices per level with many aggregates) the
+//      sort is split LSD-style: stable by j, then stable by (a, b) -- the same
+//      final order.
+//   3. one thread per (a, b) run walks it once: the inner sum restarts at each
+//      new j (B[a][j], members in order), the outer sum adds the B values in j
+//      order (C[a][b]).  Row lengths are counted on the device and scanned into
+//      indptr; the host receives the finished CSR (one synchronisation for the
+//      number of coarse entries, one for the result).
+// A row range [a0, a1) restricts steps 1-3 to those coarse rows (one rank's
+// share in ge_ptap_dist); agg(j) always uses the whole P_T.
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "ge_internal.hpp"
@@ -26,169 +41,281 @@
 namespace ge {
 namespace {
 
-__global__ void row_len_kernel(int N, const int* __restrict__ pt_ix, const int* __restrict__ ip,
-                               long long* __restrict__ len) {
+using u64 = unsigned long long;
+
+inline unsigned grid_for(long long L) { return (unsigned)((L + 255) / 256); }
+
+// bits needed for the values 0 .. x-1
+int bits_below(long long x) {
+  int b = 0;
+  while (b < 63 && (1ll << b) < x) ++b;
+  return b;
+}
+
+// heads[c] = number of aggregates a >= 1 whose first position is c; the
+// inclusive scan of heads is the aggregate of position c (empty aggregates
+// included).
+__global__ void agg_heads_kernel(int m, int n, const int* __restrict__ pt_ip,
+                                 int* __restrict__ heads) {
+  const int a = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (a < m && pt_ip[a] < n) atomicAdd(&heads[pt_ip[a]], 1);
+}
+
+__global__ void agg_vertex_kernel(int n, const int* __restrict__ pt_ix,
+                                  const int* __restrict__ agg_pos, int* __restrict__ agg_vtx) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < N) {
-    const int i = pt_ix[c];
+  if (c < n) agg_vtx[pt_ix[c]] = agg_pos[c];
+}
+
+__global__ void row_len_kernel(int P, int c0, const int* __restrict__ pt_ix,
+                               const int* __restrict__ ip, long long* __restrict__ len) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < P) {
+    const int i = pt_ix[c0 + c];
     len[c] = ip[i + 1] - ip[i];
   }
 }
 
-__global__ void agg_of_pos_kernel(int m, const int* __restrict__ pt_ip, int* __restrict__ agg_pos,
-                                  const int* __restrict__ pt_ix, int* __restrict__ agg_vtx) {
-  const int a = blockIdx.x;
-  for (int c = pt_ip[a] + threadIdx.x; c < pt_ip[a + 1]; c += blockDim.x) {
-    agg_pos[c] = a;
-    agg_vtx[pt_ix[c]] = a;
-  }
-}
-
-// One thread per P_T position; writes its member's CSR row at off[c].
-__global__ void expand_kernel(int N, const int* __restrict__ pt_ix, const int* __restrict__ agg_pos,
+// Entry t of the (c, CSR)-ordered stream: position c = last q with off[q] <= t.
+// Composite key (a - a0, b, j) with b and j in the low bits; LSD (split) mode
+// writes the j key and the (a - a0, b) key separately.
+template <bool SPLIT>
+__global__ void expand_kernel(long long L, int P, int c0, int a0, int bn, int bb,
+                              const long long* __restrict__ off, const int* __restrict__ pt_ix,
+                              const int* __restrict__ agg_pos, const int* __restrict__ agg_vtx,
                               const int* __restrict__ ip, const int* __restrict__ ix,
-                              const double* __restrict__ dx, const long long* __restrict__ off,
-                              unsigned long long* __restrict__ key, double* __restrict__ val) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  const int i = pt_ix[c];
-  const unsigned long long hi = (unsigned long long)(unsigned)agg_pos[c] << 32;
-  long long o = off[c];
-  for (int e = ip[i]; e < ip[i + 1]; ++e, ++o) {
-    key[o] = hi | (unsigned)ix[e];
-    val[o] = dx[e];
-  }
-}
-
-__global__ void head_flags_kernel(long long L, const unsigned long long* __restrict__ key,
-                                  int* __restrict__ flag) {
+                              const double* __restrict__ dx, u64* __restrict__ key,
+                              u64* __restrict__ key_hi, double* __restrict__ val) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < L) flag[t] = (t == 0 || key[t] != key[t - 1]) ? 1 : 0;
+  if (t >= L) return;
+  int lo = 0, hi = P - 1;
+  while (lo < hi) {  // largest q with off[q] <= t (rows of length 0 are skipped over)
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= t) lo = mid;
+    else hi = mid - 1;
+  }
+  const int c = c0 + lo;
+  const int i = pt_ix[c];
+  const int e = ip[i] + (int)(t - off[lo]);
+  const u64 j = (unsigned)ix[e];
+  const u64 ab = ((u64)(unsigned)(agg_pos[c] - a0) << bb) | (unsigned)agg_vtx[j];
+  if (SPLIT) {
+    key[t] = j;
+    key_hi[t] = ab;
+  } else {
+    key[t] = (ab << bn) | j;
+  }
+  val[t] = dx[e];
 }
 
-__global__ void scatter_heads_kernel(long long L, const int* __restrict__ flag,
-                                     const int* __restrict__ runid, long long* __restrict__ start) {
+// LSD second pass: the (a, b) keys in the order of the j sort.
+__global__ void gather_keys_kernel(long long L, const unsigned* __restrict__ perm,
+                                   const u64* __restrict__ key_hi, u64* __restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < L) out[t] = key_hi[perm[t]];
+}
+
+__global__ void iota_kernel(long long L, unsigned* __restrict__ v) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < L) v[t] = (unsigned)t;
+}
+
+// LSD mode: entry t of the final order is entry rp[t] of the j-sorted stream,
+// i.e. emitted entry pp[rp[t]]; its key becomes (run number, j).
+__global__ void compose_kernel(long long L, int bn, const int* __restrict__ flag,
+                               const int* __restrict__ runid, const unsigned* __restrict__ rp,
+                               const unsigned* __restrict__ pp, const u64* __restrict__ ab,
+                               const u64* __restrict__ jsorted, const double* __restrict__ vsrc,
+                               u64* __restrict__ key, double* __restrict__ val,
+                               u64* __restrict__ ab_run) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L) return;
+  const unsigned q = rp[t];
+  const int run = runid[t] - 1;
+  key[t] = ((u64)(unsigned)run << bn) | jsorted[q];
+  val[t] = vsrc[pp[q]];
+  if (flag[t]) ab_run[run] = ab[t];
+}
+
+// head of an (a, b) run: the key above the j bits changes
+__global__ void run_heads_kernel(long long L, int bn, const u64* __restrict__ key,
+                                 int* __restrict__ flag) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < L) flag[t] = (t == 0 || (key[t] >> bn) != (key[t - 1] >> bn)) ? 1 : 0;
+}
+
+__global__ void run_starts_kernel(long long L, const int* __restrict__ flag,
+                                  const int* __restrict__ runid, long long* __restrict__ start) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < L && flag[t]) start[runid[t] - 1] = t;
 }
 
-// Serial left-to-right sum of each run (the pinned order).  mul = 1.0 models
-// the multiplication by P's 1.0 entries.
-__global__ void run_sum_kernel(long long runs, long long L, const long long* __restrict__ start,
-                               const unsigned long long* __restrict__ key,
-                               const double* __restrict__ val, double mul,
-                               unsigned long long* __restrict__ okey, double* __restrict__ oval) {
+// One thread per (a, b) run (the pinned order): B[a][j] restarts at each new j
+// and adds members in P_T order; C[a][b] adds the B values in ascending j.
+// Multiplications by P's 1.0 entries are exact and left out.
+__global__ void run_sum_kernel(long long L, const int* __restrict__ nruns_p, int bn, int bb,
+                               const long long* __restrict__ start, const u64* __restrict__ key,
+                               const double* __restrict__ val, const u64* __restrict__ ab_run,
+                               int* __restrict__ out_col,
+                               double* __restrict__ out_val, int* __restrict__ row_cnt) {
   const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long runs = *nruns_p;
   if (r >= runs) return;
-  const long long b = start[r];
-  const long long e = (r + 1 < runs) ? start[r + 1] : L;
-  double s = 0.0;
-  for (long long t = b; t < e; ++t) s += val[t] * mul;
-  okey[r] = key[b];
-  oval[r] = s;
-}
-
-__global__ void rekey_kernel(long long L, const unsigned long long* __restrict__ key,
-                             const int* __restrict__ agg_vtx, unsigned long long* __restrict__ out) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < L) {
-    const unsigned long long k = key[t];
-    out[t] = (k & 0xFFFFFFFF00000000ull) | (unsigned)agg_vtx[(unsigned)(k & 0xFFFFFFFFull)];
+  const long long b0 = start[r];
+  const long long b1 = (r + 1 < runs) ? start[r + 1] : L;
+  const u64 jmask = (bn >= 64) ? ~0ull : ((1ull << bn) - 1);
+  double outer = 0.0, inner = 0.0;
+  u64 kprev = key[b0];
+  for (long long t = b0; t < b1; ++t) {
+    const u64 k = key[t];
+    if ((k & jmask) != (kprev & jmask)) {
+      outer += inner;
+      inner = 0.0;
+      kprev = k;
+    }
+    inner += val[t];
   }
+  outer += inner;
+  const u64 ab = ab_run ? ab_run[r] : key[b0] >> bn;
+  out_col[r] = (int)(ab & ((1ull << bb) - 1));
+  out_val[r] = outer;
+  atomicAdd(&row_cnt[(int)(ab >> bb)], 1);
 }
 
-inline unsigned grid_for(long long L) { return (unsigned)((L + 255) / 256); }
-
-// stable sort pairs by the low `bits` bits of the key
-void sort_pairs(hipStream_t st, DevBuf<unsigned long long>& k, DevBuf<double>& v,
-                DevBuf<unsigned long long>& k2, DevBuf<double>& v2, long long L, int end_bit) {
+template <class K, class V>
+void sort_pairs(hipStream_t st, K*& k, K*& k2, V*& v, V*& v2, long long L, int end_bit) {
   size_t tmp = 0;
-  GE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k.p, k2.p, v.p, v2.p, (int)L, 0,
-                                            end_bit, st));
+  GE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, k2, v, v2, (int)L, 0, end_bit, st));
   DevBuf<unsigned char> scratch(tmp);
-  GE_HIP(hipcub::DeviceRadixSort::SortPairs(scratch.p, tmp, k.p, k2.p, v.p, v2.p, (int)L, 0,
-                                            end_bit, st));
-  std::swap(k.p, k2.p);
-  std::swap(v.p, v2.p);
+  GE_HIP(hipcub::DeviceRadixSort::SortPairs(scratch.p, tmp, k, k2, v, v2, (int)L, 0, end_bit,
+                                            st));
+  std::swap(k, k2);
+  std::swap(v, v2);
 }
 
-// Reduce equal-key runs of (k, v)[0..L) into (k2, v2); returns the run count.
-long long reduce_runs(hipStream_t st, const DevBuf<unsigned long long>& k,
-                      const DevBuf<double>& v, DevBuf<unsigned long long>& k2,
-                      DevBuf<double>& v2, long long L) {
-  DevBuf<int> flag(L), runid(L);
-  hipLaunchKernelGGL(head_flags_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, k.p, flag.p);
+template <class T>
+void exclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
   size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, flag.p, runid.p, (int)L, st));
+  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)count, st));
   DevBuf<unsigned char> scratch(tmp);
-  GE_HIP(hipcub::DeviceScan::InclusiveSum(scratch.p, tmp, flag.p, runid.p, (int)L, st));
-  int runs = 0;
-  GE_HIP(hipMemcpyAsync(&runs, runid.p + (L - 1), sizeof(int), hipMemcpyDeviceToHost, st));
-  GE_HIP(hipStreamSynchronize(st));
-  DevBuf<long long> start(runs);
-  hipLaunchKernelGGL(scatter_heads_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, flag.p,
-                     runid.p, start.p);
-  hipLaunchKernelGGL(run_sum_kernel, dim3(grid_for(runs)), dim3(256), 0, st, (long long)runs, L,
-                     start.p, k.p, v.p, 1.0, k2.p, v2.p);
-  GE_HIP(hipGetLastError());
-  return runs;
+  GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, in, out, (int)count, st));
 }
 
-int bits_for(long long x) {
-  int b = 1;
-  while ((1ll << b) <= x) ++b;
-  return b;
+template <class T>
+void inclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
+  size_t tmp = 0;
+  GE_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, out, (int)count, st));
+  DevBuf<unsigned char> scratch(tmp);
+  GE_HIP(hipcub::DeviceScan::InclusiveSum(scratch.p, tmp, in, out, (int)count, st));
 }
 
 }  // namespace
 
 void ptap_device(ge_ctx* ctx, int n, const int* d_ip, const int* d_ix, const double* d_dx,
-                 int nnz, int m, const int* d_pt_ip, const int* d_pt_ix, ge_csr* out) {
+                 int nnz, int m, const int* h_pt_ip, const int* d_pt_ip, const int* d_pt_ix,
+                 int a0, int a1, ge_csr* out) {
   hipStream_t st = ctx->stream;
-  out->rows = out->cols = m;
-  out->indptr.assign(m + 1, 0);
+  const int R = a1 - a0;
+  out->rows = R;
+  out->cols = m;
+  out->indptr.assign(R + 1, 0);
   out->indices.clear();
   out->data.clear();
-  if (n == 0 || m == 0 || nnz == 0) return;
-  const int N = n;  // one P_T entry per fine vertex
-  DevBuf<long long> len(N), off(N);
-  DevBuf<int> agg_pos(N), agg_vtx(n);
-  hipLaunchKernelGGL(row_len_kernel, dim3(grid_for(N)), dim3(256), 0, st, N, d_pt_ix, d_ip, len.p);
-  hipLaunchKernelGGL(agg_of_pos_kernel, dim3(m), dim3(64), 0, st, m, d_pt_ip, agg_pos.p, d_pt_ix,
-                     agg_vtx.p);
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, len.p, off.p, N, st));
-  {
-    DevBuf<unsigned char> scratch(tmp);
-    GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, len.p, off.p, N, st));
+  const int c0 = h_pt_ip[a0], c1 = h_pt_ip[a1];
+  const int P = c1 - c0;
+  if (n == 0 || R == 0 || P == 0 || nnz == 0) return;
+
+  // aggregate of every P_T position and of every fine vertex
+  DevBuf<int> heads(n), agg_pos(n), agg_vtx(n);
+  GE_HIP(hipMemsetAsync(heads.p, 0, sizeof(int) * n, st));
+  if (m > 1)
+    hipLaunchKernelGGL(agg_heads_kernel, dim3(grid_for(m - 1)), dim3(256), 0, st, m, n, d_pt_ip,
+                       heads.p);
+  inclusive_scan(st, heads.p, agg_pos.p, n);
+  hipLaunchKernelGGL(agg_vertex_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, d_pt_ix,
+                     agg_pos.p, agg_vtx.p);
+
+  // emitted entries: prefix sums of the members' row lengths
+  DevBuf<long long> len(P + 1), off(P + 1);
+  GE_HIP(hipMemsetAsync(len.p + P, 0, sizeof(long long), st));
+  hipLaunchKernelGGL(row_len_kernel, dim3(grid_for(P)), dim3(256), 0, st, P, c0, d_pt_ix, d_ip,
+                     len.p);
+  exclusive_scan(st, len.p, off.p, P + 1);
+  long long L = nnz;  // every fine row appears once in P_T
+  if (a0 != 0 || a1 != m) {
+    GE_HIP(hipMemcpyAsync(&L, off.p + P, sizeof(long long), hipMemcpyDeviceToHost, st));
+    GE_HIP(hipStreamSynchronize(st));
   }
-  const long long L = nnz;
-  DevBuf<unsigned long long> k(L), k2(L);
+  if (L == 0) return;
+  GE_REQUIRE(L < (1ll << 31), "P^T A P: more than 2^31 entries in one call (shard the rows)");
+
+  const int bn = bits_below(n), bb = bits_below(m), ba = bits_below(R);
+  const bool split = ba + bb + bn > 64 || std::getenv("GE_PTAP_SPLIT_SORT") != nullptr;
+  DevBuf<u64> k(L), k2(L);
   DevBuf<double> v(L), v2(L);
-  hipLaunchKernelGGL(expand_kernel, dim3(grid_for(N)), dim3(256), 0, st, N, d_pt_ix, agg_pos.p,
-                     d_ip, d_ix, d_dx, off.p, k.p, v.p);
+  u64 *kp = k.p, *kq = k2.p;
+  double *vp = v.p, *vq = v2.p;
+  DevBuf<u64> ab_run;  // split mode: (a, b) of each run
+  if (!split) {
+    hipLaunchKernelGGL(expand_kernel<false>, dim3(grid_for(L)), dim3(256), 0, st, L, P, c0, a0,
+                       bn, bb, off.p, d_pt_ix, agg_pos.p, agg_vtx.p, d_ip, d_ix, d_dx, kp,
+                       nullptr, vp);
+    GE_HIP(hipGetLastError());
+    sort_pairs(st, kp, kq, vp, vq, L, std::max(1, ba + bb + bn));
+  } else {
+    // LSD: stable by j, then stable by (a, b).  The (a, b) pairs are then replaced
+    // by their dense run number (< L < 2^31), so (run, j) fits 64 bits again.
+    DevBuf<u64> khi(L);
+    DevBuf<unsigned> perm(L), perm2(L), rank(L), rank2(L);
+    hipLaunchKernelGGL(expand_kernel<true>, dim3(grid_for(L)), dim3(256), 0, st, L, P, c0, a0, bn,
+                       bb, off.p, d_pt_ix, agg_pos.p, agg_vtx.p, d_ip, d_ix, d_dx, kp, khi.p, vp);
+    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, perm.p);
+    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, rank.p);
+    GE_HIP(hipGetLastError());
+    unsigned *pp = perm.p, *pq = perm2.p, *rp = rank.p, *rq = rank2.p;
+    sort_pairs(st, kp, kq, pp, pq, L, std::max(1, bn));  // kp[q]: j of entry pp[q], j ascending
+    u64 *hs = kq, *ht = khi.p;              // (kq is free now)
+    hipLaunchKernelGGL(gather_keys_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, pp, khi.p, hs);
+    // khi is read by the gather before the sort below reuses it as scratch (same stream)
+    sort_pairs(st, hs, ht, rp, rq, L, std::max(1, ba + bb));  // hs[t]: (a, b) of stream entry rp[t]
+    DevBuf<int> flag(L), runid(L);
+    hipLaunchKernelGGL(run_heads_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, 0, hs, flag.p);
+    inclusive_scan(st, flag.p, runid.p, L);
+    ab_run.alloc(L);
+    hipLaunchKernelGGL(compose_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, bn, flag.p,
+                       runid.p, rp, pp, hs, kp, vp, ht, vq, ab_run.p);
+    GE_HIP(hipGetLastError());
+    std::swap(kp, ht);  // composed keys (ht was the (a, b) sort's scratch)
+    std::swap(vp, vq);
+  }
+
+  // (a, b) runs and their serial sums
+  DevBuf<int> flag(L), runid(L), row_cnt(R + 1);
+  DevBuf<long long> start(L);
+  hipLaunchKernelGGL(run_heads_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, bn, kp, flag.p);
+  inclusive_scan(st, flag.p, runid.p, L);
+  GE_HIP(hipMemsetAsync(row_cnt.p, 0, sizeof(int) * (R + 1), st));
+  hipLaunchKernelGGL(run_starts_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, flag.p, runid.p,
+                     start.p);
+  DevBuf<int> ocol(L);
+  DevBuf<double> oval(L);
+  hipLaunchKernelGGL(run_sum_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, runid.p + (L - 1),
+                     bn, bb, start.p, kp, vp, ab_run.p, ocol.p, oval.p, row_cnt.p);
   GE_HIP(hipGetLastError());
-  const int key_bits = 32 + bits_for(m);
-  sort_pairs(st, k, v, k2, v2, L, key_bits);  // result in k, v
-  long long nb = reduce_runs(st, k, v, k2, v2, L);  // B in k2, v2
-  std::swap(k.p, k2.p);
-  std::swap(v.p, v2.p);  // B in k, v
-  hipLaunchKernelGGL(rekey_kernel, dim3(grid_for(nb)), dim3(256), 0, st, nb, k.p, agg_vtx.p, k2.p);
-  std::swap(k.p, k2.p);  // rekeyed B in k
-  sort_pairs(st, k, v, k2, v2, nb, key_bits);
-  long long nc = reduce_runs(st, k, v, k2, v2, nb);  // C in k2, v2
-  std::vector<unsigned long long> hk(nc);
-  out->data.resize(nc);
-  GE_HIP(hipMemcpyAsync(hk.data(), k2.p, sizeof(unsigned long long) * nc, hipMemcpyDeviceToHost, st));
-  GE_HIP(hipMemcpyAsync(out->data.data(), v2.p, sizeof(double) * nc, hipMemcpyDeviceToHost, st));
+  DevBuf<int> indptr(R + 1);
+  exclusive_scan(st, row_cnt.p, indptr.p, R + 1);
+  int nc = 0;
+  GE_HIP(hipMemcpyAsync(&nc, runid.p + (L - 1), sizeof(int), hipMemcpyDeviceToHost, st));
   GE_HIP(hipStreamSynchronize(st));
   out->indices.resize(nc);
-  for (long long t = 0; t < nc; ++t) {
-    const int a = (int)(hk[t] >> 32);
-    out->indices[t] = (int)(hk[t] & 0xFFFFFFFFull);
-    out->indptr[a + 1]++;
-  }
-  for (int a = 0; a < m; ++a) out->indptr[a + 1] += out->indptr[a];
+  out->data.resize(nc);
+  GE_HIP(hipMemcpyAsync(out->indptr.data(), indptr.p, sizeof(int) * (R + 1),
+                        hipMemcpyDeviceToHost, st));
+  GE_HIP(hipMemcpyAsync(out->indices.data(), ocol.p, sizeof(int) * nc, hipMemcpyDeviceToHost,
+                        st));
+  GE_HIP(hipMemcpyAsync(out->data.data(), oval.p, sizeof(double) * nc, hipMemcpyDeviceToHost,
+                        st));
+  GE_HIP(hipStreamSynchronize(st));
 }
 
 }  // namespace ge

@@ -92,6 +92,10 @@ __device__ __forceinline__ void sym_step(int sg, int lane, int ncols, double* ou
   // and the absorbed columns' sums are dead values.
   double t[D];
   rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
+  if (!SHARED && DIAG && sg - lane == lane) {  // the `/` form skips the self pair (ge_pair.hpp)
+#pragma unroll
+    for (int k = 0; k < D; ++k) t[k] = 0.0;
+  }
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     racc[k] = racc[k] + t[k];
@@ -207,7 +211,8 @@ __device__ __forceinline__ void rows_block(int lane, int base, int s, int A, con
         rep_pair<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
     } else {
       for (int jj = 0; jj < cnt; ++jj)
-        rep_pair<D, false, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
+        rep_pair_fb<D, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel,
+                                  j0 + jj == 64 * A + lane, acc);
     }
   }
   if (rv) {

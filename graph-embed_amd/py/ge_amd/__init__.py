@@ -115,6 +115,33 @@ _SIGS = {
                                    ctypes.POINTER(_vp)]),
     "ge_largest_component": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p,
                                             ctypes.POINTER(_vp)]),
+    # multi-GPU (ge_dist.hip)
+    "ge_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "ge_comm_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                      ctypes.POINTER(_vp)]),
+    "ge_comm_create_transport": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp,
+                                                ctypes.POINTER(_vp)]),
+    "ge_comm_info": (ctypes.c_int, [_vp, _ip, _ip, _ip]),
+    "ge_comm_destroy": (ctypes.c_int, [_vp]),
+    "ge_row_shard": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _ip, _ip, _ip]),
+    "ge_allgather_coords": (ctypes.c_int, [_vp, _vp, ctypes.c_longlong, ctypes.c_int]),
+    "ge_assign_aggregates": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _vp, ctypes.c_int,
+                                            _i32p]),
+    "ge_allgather_members": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
+                                            _i32p]),
+    "ge_force_atlas_dist": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
+                                           _f64p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(FaParams)]),
+    "ge_force_atlas_ml_dist": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p,
+                                              ctypes.c_int, _i32p, _i32p, _i32p, _f64p, _f64p,
+                                              _f64p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(FaParams)]),
+    "ge_ptap_dist": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int, _i32p,
+                                    _i32p, ctypes.POINTER(_vp)]),
+    "ge_embed_dist": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _i32p,
+                                     _f64p, _i32p, _i32p, _i32p, _i32p, _i32p, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.POINTER(FaParams), _f64p]),
 }
 
 _lib = None
@@ -270,6 +297,156 @@ class Context:
 
     def fa_plan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw):
         return FaPlan(self, n, nnz, d_ip, d_ix, d_dx, dim, row_begin, row_end, **kw)
+
+
+_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _vp, ctypes.c_ulonglong)
+
+
+class _Transport(ctypes.Structure):
+    _fields_ = [("user", _vp), ("allgather", _ALLGATHER_FN)]
+
+
+def _torch_allgather(send, recv, nbytes):
+    """ge_transport.allgather over the default torch.distributed group (gloo):
+    host byte blocks, rank-major."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    if nbytes == 0:
+        dist.barrier()
+        return
+    src = np.ctypeslib.as_array((ctypes.c_ubyte * nbytes).from_address(send))
+    dst = np.ctypeslib.as_array((ctypes.c_ubyte * (nbytes * world)).from_address(recv))
+    outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(outs, torch.from_numpy(src.copy()))
+    for r, t in enumerate(outs):
+        dst[r * nbytes:(r + 1) * nbytes] = t.numpy()
+
+
+class Comm:
+    """ge_comm: the library's communicator for one rank (one process per GPU).
+
+    backend "rccl": ncclCommInitRank inside libge; the 128-byte unique id made by
+    rank 0 (unique_id()) must be handed to every rank (e.g. broadcast_object_list).
+    backend "transport": the library's collectives call back into Python, which
+    all-gathers host blocks over torch.distributed's default group (gloo) -- the
+    multi-process rehearsal on one GPU and the CPU-side tests."""
+
+    def __init__(self, ctx, nranks, rank, backend="rccl", uid=None):
+        self.ctx, self.nranks, self.rank = ctx, nranks, rank
+        h = _vp()
+        if backend == "rccl":
+            assert uid is not None and len(uid) == 128
+            _check(lib().ge_comm_create(ctx.h, nranks, rank, bytes(uid), ctypes.byref(h)))
+        else:
+            def cb(user, send, recv, nbytes):
+                try:
+                    _torch_allgather(send, recv, int(nbytes))
+                    return 0
+                except Exception:  # reported to the library as a failed collective
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+            self._cb = _ALLGATHER_FN(cb)  # kept alive with the communicator
+            self._tp = _Transport(None, self._cb)
+            _check(lib().ge_comm_create_transport(ctx.h, nranks, rank,
+                                                  ctypes.cast(ctypes.byref(self._tp), _vp),
+                                                  ctypes.byref(h)))
+        self.h = h
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().ge_comm_unique_id(buf))
+        return buf.raw
+
+    def info(self):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().ge_comm_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, bool(c.value)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ge_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def allgather_coords(self, d_x, rows_per_rank, dim):
+        _check(lib().ge_allgather_coords(self.h, _vp(d_x), rows_per_rank, dim))
+
+    def allgather_members(self, d_x, dim, PT, owner):
+        pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+        pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+        _check(lib().ge_allgather_members(self.h, _vp(d_x), dim, len(pip) - 1, pip, pix,
+                                          np.ascontiguousarray(owner, dtype=np.int32)))
+
+    def force_atlas(self, A, dim, coords=None, iterations=100000, **kw):
+        ip, ix, dx = _csr(A)
+        n = len(ip) - 1
+        X = np.zeros((n, dim)) if coords is None else np.array(coords, dtype=np.float64)
+        X = np.ascontiguousarray(X)
+        p = params(**kw)
+        _check(lib().ge_force_atlas_dist(self.h, n, ip, ix, dx, dim, X.reshape(-1),
+                                         int(coords is None), iterations, ctypes.byref(p)))
+        return X
+
+    def force_atlas_ml(self, A, PT, vertex_A, coords_A, r_A, dim, iterations=10, **kw):
+        ip, ix, dx = _csr(A)
+        pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+        pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+        n = len(ip) - 1
+        X = np.zeros((n, dim))
+        p = params(**kw)
+        _check(lib().ge_force_atlas_ml_dist(
+            self.h, n, ip, ix, dx, len(pip) - 1, pip, pix,
+            np.ascontiguousarray(vertex_A, dtype=np.int32),
+            np.ascontiguousarray(coords_A, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(r_A, dtype=np.float64), X.reshape(-1), dim, iterations,
+            ctypes.byref(p)))
+        return X
+
+    def ptap(self, A, PT):
+        ip, ix, dx = _csr(A)
+        pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+        pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+        h = _vp()
+        _check(lib().ge_ptap_dist(self.h, len(ip) - 1, ip, ix, dx, len(pip) - 1, pip, pix,
+                                  ctypes.byref(h)))
+        return _take_csr(h)
+
+    def embed(self, As, hier, dim, base_iterations=100000, ml_iterations=100,
+              print_progress=False, **kw):
+        parts = concat_levels(As, hier)
+        out = np.empty((len(As[0][0]) - 1, dim))
+        p = params(**kw)
+        _check(lib().ge_embed_dist(self.h, len(hier), *parts, dim, base_iterations,
+                                   ml_iterations, int(print_progress), ctypes.byref(p),
+                                   out.reshape(-1)))
+        return out
+
+
+def assign_aggregates(PT, indptr, nranks):
+    """ge_assign_aggregates: the rank of every aggregate (LPT by s(s-1) + the
+    members' CSR entries when indptr is given)."""
+    pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+    pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+    owner = np.empty(len(pip) - 1, dtype=np.int32)
+    ipa = None if indptr is None else np.ascontiguousarray(indptr, dtype=np.int32)
+    _check(lib().ge_assign_aggregates(len(pip) - 1, pip, pix,
+                                      None if ipa is None else ipa.ctypes.data_as(_vp), nranks,
+                                      owner))
+    return owner
+
+
+def row_shard(n, nranks, rank):
+    a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().ge_row_shard(n, nranks, rank, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+    return a.value, b.value, c.value
 
 
 class FamlPlan:

@@ -206,6 +206,82 @@ int ge_radius_step(int m, double* coords_A, double* r_A, int dim, int coarse_is_
                    const int* ptc_indptr, const int* ptc_indices, const double* coords_Ac,
                    const double* r_Ac, const int* ac_indptr, const int* ac_indices);
 
+/* ---- multi-GPU: one process per GPU, a communicator per context ----
+ * The reference has no multi-GPU path (it is OpenMP on one node); these entry
+ * points shard the same computations across ranks and return
+ * the same bits on every rank as the single-GPU calls:
+ *   - forceAtlas: contiguous row shards + one all-gather of the fp64
+ *     coordinates per iteration (include/forceatlas.hpp:146-270 reads all
+ *     coordinates of the previous iteration, nothing else is global: :228, :242);
+ *     levels small enough for the fused single-launch kernels run as replicas.
+ *   - forceAtlasMultilevel: aggregates dealt to ranks by cost (longest
+ *     processing time first), no exchange during the iterations (:454, :462 read
+ *     only the frozen coarse coordinates), one all-gather of the members'
+ *     coordinates at the end.
+ *   - P^T A P: coarse rows dealt to ranks in contiguous blocks of equal expanded
+ *     work, one all-gather of the coarse rows.
+ * A communicator is RCCL (ncclCommInitRank over xGMI: ge_comm_unique_id on
+ * rank 0, shipped to the others out of band) or a caller transport (host
+ * all-gather callback, e.g. MPI or gloo; data are staged through host memory).
+ * Every rank passes the same inputs; collective calls must be made by all ranks
+ * in the same order. */
+#define GE_COMM_ID_BYTES 128
+typedef struct ge_comm ge_comm;
+typedef struct ge_transport {
+  void* user;
+  /* All-gather of equal blocks: recv (nranks * bytes, rank-major) receives every
+   * rank's `bytes` bytes of send.  Host pointers.  Returns 0 on success. */
+  int (*allgather)(void* user, const void* send, void* recv, unsigned long long bytes);
+} ge_transport;
+
+int ge_comm_unique_id(unsigned char* id /* GE_COMM_ID_BYTES */);
+/* RCCL communicator on the context's device; collectives run on its stream. */
+int ge_comm_create(ge_ctx* ctx, int nranks, int rank, const unsigned char* id, ge_comm** out);
+int ge_comm_create_transport(ge_ctx* ctx, int nranks, int rank, const ge_transport* t,
+                             ge_comm** out);
+int ge_comm_info(const ge_comm* comm, int* nranks, int* rank, int* is_rccl);
+int ge_comm_destroy(ge_comm* comm);
+
+/* Row shard of rank `rank`: rows [*row_begin, *row_end) of n, blocks of
+ * *rows_per_rank = ceil(n / nranks) rows (coordinate buffers hold
+ * nranks * rows_per_rank rows so every rank's block has the same size). */
+int ge_row_shard(int n, int nranks, int rank, int* row_begin, int* row_end, int* rows_per_rank);
+/* In-place all-gather of rank blocks of a device coordinate array
+ * d_x[nranks * rows_per_rank * dim]: rank r contributes rows
+ * [r * rows_per_rank, (r + 1) * rows_per_rank). */
+int ge_allgather_coords(ge_comm* comm, double* d_x, long long rows_per_rank, int dim);
+/* Deal aggregates to ranks by cost s(s-1) + (CSR entries of the members, when
+ * indptr != NULL): descending cost (ties: lower id) to the least-loaded rank
+ * (ties: lower rank).  owner[m] receives each aggregate's rank.  Host only. */
+int ge_assign_aggregates(int m, const int* pt_indptr, const int* pt_indices, const int* indptr,
+                         int nranks, int* owner);
+/* After every rank wrote the coordinates of the members of its own aggregates
+ * into d_x (n * dim, fine-vertex order; e.g. ge_faml_plan_run of a subset plan),
+ * every rank holds all of them.  h_owner: ge_assign_aggregates' result;
+ * h_pt_indptr / h_pt_indices: P_T on the host. */
+int ge_allgather_members(ge_comm* comm, double* d_x, int dim, int m, const int* h_pt_indptr,
+                         const int* h_pt_indices, const int* h_owner);
+
+/* Sharded forms of ge_force_atlas, ge_force_atlas_ml, ge_ptap and ge_embed (same
+ * arguments, the context is the communicator's).  Results are identical on
+ * every rank and bit-identical to the single-GPU calls. */
+int ge_force_atlas_dist(ge_comm* comm, int n, const int* indptr, const int* indices,
+                        const double* data, int dim, double* coords, int init_random,
+                        int iterations, const ge_fa_params* p);
+int ge_force_atlas_ml_dist(ge_comm* comm, int n, const int* indptr, const int* indices,
+                           const double* data, int m, const int* pt_indptr,
+                           const int* pt_indices, const int* vertex_A, const double* coords_A,
+                           const double* r_A, double* coords, int dim, int iterations,
+                           const ge_fa_params* p);
+int ge_ptap_dist(ge_comm* comm, int n, const int* indptr, const int* indices, const double* data,
+                 int m, const int* pt_indptr, const int* pt_indices, ge_csr** out);
+int ge_embed_dist(ge_comm* comm, int levels, const int* a_n, const int* a_off,
+                  const int* a_nz_off, const int* a_indptr, const int* a_indices,
+                  const double* a_data, const int* p_rows, const int* p_off,
+                  const int* p_nz_off, const int* p_indptr, const int* p_indices, int dim,
+                  int base_iterations, int ml_iterations, int print_progress,
+                  const ge_fa_params* p, double* coords_out);
+
 /* The reference's initial-coordinate stream: the first `count` values of
  * uniform_real_distribution<double>(-1,1) over mt19937(seed) (libstdc++). */
 int ge_uniform_stream(unsigned seed, long long count, double* out);

@@ -91,3 +91,62 @@ def test_ptap_and_embed_degenerate(ctx, oracle, name):
     X = ctx.embed(As, hier, 2, seed=5, base_iterations=2000, ml_iterations=50)
     want = oracle.embed(As, hier, 2, seed=5, base_iterations=2000, ml_iterations=50)
     assert np.array_equal(X, want)
+
+
+# repel = 1e299 puts every pair outside the shared-reciprocal domain (the `/`
+# path), and the self pair's cij / eps^2 overflows to inf: the reference skips
+# j == i (include/forceatlas.hpp:151), so the kernels must too (a 0 * inf term
+# would turn the row's sum into NaN).  One iteration stays finite.
+HUGE_REPEL = 1e299
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,env", [
+    (40, {"GE_SMALL_MAX": "512"}),                         # one workgroup
+    (300, {"GE_SMALL_MAX": "0"}),                          # fa_grouped_step
+    (4000, {}),                                            # fa_grouped_stream
+    (3000, {"GE_STREAM_MAX": "0", "GE_SMALL_MAX": "0"}),   # fa_repulse_strict + rows
+])
+def test_fa_self_pair_overflow(ctx, oracle, monkeypatch, n, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    A = G.rmat(n, 4 * n, seed=n)
+    X0 = G.random_coords(n, 3, seed=1)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=1, repel=HUGE_REPEL)
+    got = ctx.force_atlas(A, 3, coords=X0, iterations=1, repel=HUGE_REPEL)
+    assert np.isfinite(want).all()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sym", ["1", "0"])
+def test_faml_self_pair_overflow(ctx, oracle, monkeypatch, sym):
+    """Multilevel: resident packs, the symmetric kernel's diagonal tiles and row
+    blocks, and the ordered-pair streamed kernel, all on the `/` path."""
+    monkeypatch.setenv("GE_FAML_SYM", sym)
+    sizes = [2600, 700, 257, 90, 5, 1]
+    n = sum(sizes)
+    A = G.submatrix(G.rmat(n, 6 * n, seed=2), np.arange(n))
+    ip = np.cumsum([0] + sizes).astype(np.int32)
+    PT = (ip, np.arange(n, dtype=np.int32))
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, 3, seed=m)
+    rA = np.random.RandomState(m).uniform(0.1, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=1, seed=3, repel=HUGE_REPEL)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=1, seed=3, repel=HUGE_REPEL)
+    assert np.isfinite(want).all()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_fa_flat_dimension_signed_zeros(ctx, oracle):
+    """Every vertex has the same third coordinate: every repulsion and attraction
+    term of that dimension is +-0, so the sums depend on starting from +0."""
+    n = 2000
+    A = G.rmat(n, 5 * n, seed=9)
+    X0 = G.random_coords(n, 3, seed=4)
+    X0[:, 2] = 0.0
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=5)
+    got = ctx.force_atlas(A, 3, coords=X0, iterations=5)
+    assert np.array_equal(got, want)

@@ -123,3 +123,34 @@ def test_assign_aggregates_partition_and_balance():
         assert max(loads) <= cost.sum() / world + cost.max()  # LPT bound
         again, _ = assign_aggregates(cost, world)
         assert all(np.array_equal(a, b) for a, b in zip(owned, again))
+
+
+def test_library_assign_aggregates_matches_harness():
+    """libge's ge_assign_aggregates (the deal inside ge_force_atlas_ml_dist) gives
+    every aggregate the rank the harness's LPT deal gives it (host-only call)."""
+    import ge_amd as ge
+    from ge_amd.dist import aggregate_cost, assign_aggregates
+    A = G.largest_component(G.rmat(3000, 20000, seed=3))
+    import oracle_lib as O
+    O.build()
+    PT = O.partition(A, 0.125)[0]
+    for world in (1, 2, 3, 8):
+        owned, _ = assign_aggregates(aggregate_cost(PT[0], A[0], PT[1]), world)
+        want = np.empty(PT[2], dtype=np.int32)
+        for r, o in enumerate(owned):
+            want[o] = r
+        assert np.array_equal(ge.assign_aggregates(PT, A[0], world), want)
+        owned, _ = assign_aggregates(aggregate_cost(PT[0]), world)
+        for r, o in enumerate(owned):
+            want[o] = r
+        assert np.array_equal(ge.assign_aggregates(PT, None, world), want)
+
+
+def test_library_row_shard_matches_harness():
+    import ge_amd as ge
+    from ge_amd.dist import row_shards
+    for n in (1, 7, 1000, 1000001):
+        for world in (1, 2, 3, 8):
+            chunk, sh = row_shards(n, world)
+            for r in range(world):
+                assert ge.row_shard(n, world, r) == (sh[r][0], sh[r][1], chunk)

@@ -48,3 +48,58 @@ def test_dropin_driver_c1(tmp_path, golden, multilevel_api):
     assert "embedding layer" in r.stdout  # the reference's progress lines
     X = np.fromfile(out, dtype=np.float64).reshape(-1, 2)
     assert np.array_equal(X, g["coords"])
+
+
+def _read_csrs(path, count):
+    buf = open(path, "rb").read()
+    off, out = 0, []
+    for _ in range(count):
+        n, nnz = np.frombuffer(buf, np.int32, 2, off)
+        off += 8
+        ip = np.frombuffer(buf, np.int32, n + 1, off); off += 4 * (n + 1)
+        ix = np.frombuffer(buf, np.int32, nnz, off); off += 4 * nnz
+        dx = np.frombuffer(buf, np.float64, nnz, off); off += 8 * nnz
+        out.append((ip, ix, dx))
+    return out
+
+
+@pytest.mark.parametrize("self_loops", [False, True])
+def test_laplacian_helpers(tmp_path, self_loops):
+    """partition::identity / toLaplacian / fromLaplacian (src/matrixutils.cpp:16-98):
+    L's rows are A's rows negated with the diagonal (serial row sum) inserted before
+    the first column > i; fromLaplacian(toLaplacian(A)) == A without self-loops."""
+    import scipy.sparse as sp
+    import graphs as G
+    exe = str(tmp_path / "lap")
+    subprocess.check_call(["g++", "-std=c++14", "-O2", "-Wall", "-Wextra", "-Werror",
+                           f"-I{PKG}/include", f"-I{PKG}/compat",
+                           os.path.join(HERE, "cpp", "laplacian.cpp"), "-o", exe])
+    ip, ix, dx = G.rmat(300, 1500, seed=4)
+    M = sp.csr_matrix((dx * np.random.RandomState(1).uniform(0.5, 2, len(dx)), ix, ip),
+                      shape=(300, 300))
+    M = M + M.T
+    if self_loops:
+        M = M + sp.diags((np.arange(300) % 3 == 0).astype(np.float64) * 2.0)
+    M = sp.csr_matrix(M)
+    M.sort_indices()
+    A = (M.indptr.astype(np.int32), M.indices.astype(np.int32), M.data.astype(np.float64))
+    write_csr(str(tmp_path / "a.bin"), A)
+    subprocess.check_call([exe, str(tmp_path / "a.bin"), str(tmp_path / "o.bin")])
+    I, L, B = _read_csrs(str(tmp_path / "o.bin"), 3)
+    assert np.array_equal(I[0], np.arange(301)) and np.array_equal(I[1], np.arange(300))
+    assert (I[2] == 1.0).all()
+    # structure: one extra (diagonal) entry per row, inserted before the first column > i
+    assert np.array_equal(np.diff(L[0]), np.diff(A[0]) + 1)
+    for i in range(300):
+        cols, vals = A[1][A[0][i]:A[0][i + 1]], A[2][A[0][i]:A[0][i + 1]]
+        deg = 0.0
+        for v in vals:  # the reference's serial row sum
+            deg += v
+        k = int(np.searchsorted(cols, i, side="right"))
+        want_c = np.concatenate([cols[:k], [i], cols[k:]])
+        want_v = np.concatenate([-vals[:k], [deg], -vals[k:]])
+        got = slice(L[0][i], L[0][i + 1])
+        assert np.array_equal(L[1][got], want_c) and np.array_equal(L[2][got], want_v)
+    if not self_loops:
+        for a, b in zip(B, A):
+            assert np.array_equal(a, b)
