@@ -182,6 +182,12 @@ void radius_step(int m, double* cA, double* rA, int dim, bool base, int mc, cons
 
 }  // namespace
 
+void radius_step_host(int m, double* cA, double* rA, int dim, bool base, int mc, const int* PIc,
+                      const int* PJc, const double* cAc, const double* rAc, const int* AcI,
+                      const int* AcJ) {
+  radius_step(m, cA, rA, dim, base, mc, PIc, PJc, cAc, rAc, AcI, AcJ);
+}
+
 // ---------------------------------------------------------------------------
 // multilevel FA on the device from host arrays
 
@@ -275,6 +281,8 @@ void embed_impl(ge_ctx* ctx, ge_comm* comm, int levels, const int* a_n, const in
 
   const int L = levels;
   const bool prof = std::getenv("GE_PROFILE_EMBED") != nullptr;
+  const char* rh = std::getenv("GE_RADIUS_HOST");
+  const bool radius_host = rh && *rh && *rh != '0';
   auto clk = [] { return std::chrono::steady_clock::now(); };
   auto secs = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count(); };
   if (print_progress) std::cout << "embedding layer " << L + 1 << ": getting base coords" << std::endl;
@@ -291,10 +299,19 @@ void embed_impl(ge_ctx* ctx, ge_comm* comm, int levels, const int* a_n, const in
     const bool base = (l + 1 == L);
     std::vector<double> rA(m);
     auto t1 = clk();
-    radius_step(m, coarse.data(), rA.data(), dim, base, base ? 0 : p_rows[l + 1],
-                base ? nullptr : Pip(l + 1), base ? nullptr : Pix(l + 1),
-                base ? nullptr : cAc.data(), base ? nullptr : r_coarse.data(), Aip(l + 1),
-                Aix(l + 1));
+    // on the device (ge_radius.hip) unless GE_RADIUS_HOST is set or a zero
+    // distance needs the serial replay
+    const int mc = base ? 0 : p_rows[l + 1];
+    const int* PIc = base ? nullptr : Pip(l + 1);
+    const int* PJc = base ? nullptr : Pix(l + 1);
+    const double* cAcp = base ? nullptr : cAc.data();
+    const double* rAcp = base ? nullptr : r_coarse.data();
+    if (!radius_host && radius_step_device(ctx, m, coarse.data(), rA.data(), dim, base, mc, PIc,
+                                           PJc, cAcp, rAcp, Aip(l + 1), Aix(l + 1))) {
+    } else {
+      radius_step(m, coarse.data(), rA.data(), dim, base, mc, PIc, PJc, cAcp, rAcp, Aip(l + 1),
+                  Aix(l + 1));
+    }
     auto t2 = clk();
     std::vector<int> vA(a_n[l]);
     for (int a = 0; a < m; ++a)

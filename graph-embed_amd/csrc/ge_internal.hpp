@@ -174,6 +174,15 @@ void faml_host(ge_ctx* ctx, int n, const int* ip, const int* ix, const double* d
                const int* pip, const int* pix, const int* vA, const double* cA,
                const double* rA, double* X, int dim, int iterations, const ge_fa_params& p);
 void normalize_host(double* X, int n, int dim);
+// radius step (src/embed.cpp:615-777): host replay of the serial event loop
+// (ge_host.cpp) and the device rounds (ge_radius.hip; false: a zero distance,
+// the caller must use the host version)
+void radius_step_host(int m, double* cA, double* rA, int dim, bool base, int mc, const int* PIc,
+                      const int* PJc, const double* cAc, const double* rAc, const int* AcI,
+                      const int* AcJ);
+bool radius_step_device(ge_ctx* ctx, int m, double* cA, double* rA, int dim, bool base, int mc,
+                        const int* PIc, const int* PJc, const double* cAc, const double* rAc,
+                        const int* AcI, const int* AcJ);
 void fa_host_dist(ge_comm* comm, int n, const int* ip, const int* ix, const double* dx, int dim,
                   double* X, bool init_random, int iterations, const ge_fa_params& p);
 void faml_host_dist(ge_comm* comm, int n, const int* ip, const int* ix, const double* dx, int m,

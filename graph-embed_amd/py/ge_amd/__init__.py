@@ -115,6 +115,9 @@ _SIGS = {
                                    ctypes.POINTER(_vp)]),
     "ge_largest_component": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _f64p,
                                             ctypes.POINTER(_vp)]),
+    "ge_radius_step_device": (ctypes.c_int, [_vp, ctypes.c_int, _f64p, _f64p, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
+                                             _vp, _ip]),
     # multi-GPU (ge_dist.hip)
     "ge_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "ge_comm_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
@@ -289,6 +292,32 @@ class Context:
         _check(lib().ge_embed(self.h, len(hier), *parts, dim, base_iterations, ml_iterations,
                               int(print_progress), ctypes.byref(p), out.reshape(-1)))
         return out
+
+    def radius_step(self, coords_A, dim, coarse_is_base, PTc=None, coords_Ac=None, r_Ac=None,
+                    Ac=None):
+        """ge_radius_step_device: returns (r_A, coords_A after the rescale, ran_on_device)."""
+        cA = np.array(coords_A, dtype=np.float64, copy=True).reshape(-1)
+        m = cA.size // dim
+        rA = np.zeros(m)
+        keep = []
+
+        def ptr(a, dt):
+            if a is None:
+                return None
+            a = np.ascontiguousarray(a, dtype=dt)
+            keep.append(a)
+            return a.ctypes.data_as(_vp)
+
+        used = ctypes.c_int(-1)
+        mc = 0 if PTc is None else len(PTc[0]) - 1
+        _check(lib().ge_radius_step_device(
+            self.h, m, cA, rA, dim, int(coarse_is_base), mc,
+            ptr(None if PTc is None else PTc[0], np.int32),
+            ptr(None if PTc is None else PTc[1], np.int32),
+            ptr(coords_Ac, np.float64), ptr(r_Ac, np.float64),
+            ptr(None if Ac is None else Ac[0], np.int32),
+            ptr(None if Ac is None else Ac[1], np.int32), ctypes.byref(used)))
+        return rA, cA.reshape(m, dim), bool(used.value)
 
     def selftest_math(self, samples=1 << 24, seed=1):
         bad = ctypes.c_longlong()

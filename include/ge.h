@@ -206,6 +206,15 @@ int ge_radius_step(int m, double* coords_A, double* r_A, int dim, int coarse_is_
                    const int* ptc_indptr, const int* ptc_indices, const double* coords_Ac,
                    const double* r_Ac, const int* ac_indptr, const int* ac_indices);
 
+/* The same step on the device (graph-embed_amd/csrc/ge_radius.hip): the events
+ * pop in parallel rounds with the serial loop's result bits.  When an event
+ * distance is 0 (coincident coarse coordinates) the host loop runs instead;
+ * *used_device (may be NULL) tells which ran.  embed uses this form. */
+int ge_radius_step_device(ge_ctx* ctx, int m, double* coords_A, double* r_A, int dim,
+                          int coarse_is_base, int mc, const int* ptc_indptr,
+                          const int* ptc_indices, const double* coords_Ac, const double* r_Ac,
+                          const int* ac_indptr, const int* ac_indices, int* used_device);
+
 /* ---- multi-GPU: one process per GPU, a communicator per context ----
  * The reference has no multi-GPU path (it is OpenMP on one node); these entry
  * points shard the same computations across ranks and return
