@@ -118,6 +118,8 @@ _SIGS = {
     "ge_radius_step_device": (ctypes.c_int, [_vp, ctypes.c_int, _f64p, _f64p, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, _vp,
                                              _vp, _ip]),
+    "ge_embed_via_minimization": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, ctypes.c_int, _f64p,
+                                                 ctypes.c_int, ctypes.c_uint, ctypes.c_int]),
     # multi-GPU (ge_dist.hip)
     "ge_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "ge_comm_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
@@ -656,6 +658,18 @@ def radius_step(coords_A, dim, coarse_is_base, PTc=None, coords_Ac=None, r_Ac=No
         ptr(coords_Ac, np.float64), ptr(r_Ac, np.float64),
         ptr(None if Ac is None else Ac[0], np.int32), ptr(None if Ac is None else Ac[1], np.int32)))
     return rA, cA.reshape(m, dim)
+
+
+def embed_via_minimization(A, dim, coords=None, iterations=10, seed=12345):
+    """partition::embedViaMinimization(A, d, coords, ITER) (src/embed.cpp:341-559);
+    coords=None draws the reference's random start from mt19937(seed)."""
+    ip, ix, _ = _csr(A)
+    n = len(ip) - 1
+    X = np.zeros((n, dim)) if coords is None else np.array(coords, dtype=np.float64)
+    X = np.ascontiguousarray(X)
+    _check(lib().ge_embed_via_minimization(n, ip, ix, dim, X.reshape(-1), int(coords is None),
+                                           seed, iterations))
+    return X
 
 
 def uniform_stream(seed, count):

@@ -291,6 +291,19 @@ int ge_embed_dist(ge_comm* comm, int levels, const int* a_n, const int* a_off,
                   int base_iterations, int ml_iterations, int print_progress,
                   const ge_fa_params* p, double* coords_out);
 
+/* ---- alternative embedder ----
+ * Replaces partition::embedViaMinimization(A, d, coords, ITER) (include/embed.hpp:22-23,
+ * src/embed.cpp:341-559): `iterations` Gauss-Seidel sweeps of a per-vertex line
+ * search towards the 2d unit directions, then centring and scaling.  coords:
+ * n*dim in/out; init_random != 0 first draws U(-1,1) from mt19937(seed) (the
+ * reference's empty-coords branch, :353-361).  Edge weights are not read (the
+ * reference ignores them).  Host code (off the embed path; the line searches are
+ * chains of serial n-term sums); the 2d directions run on OpenMP threads.
+ * anyToMultilevel / embedVia / embedViaMultilevel (src/embed.cpp:23-338) are
+ * header-only in graph-embed_amd/include/embed.hpp on top of this ABI. */
+int ge_embed_via_minimization(int n, const int* indptr, const int* indices, int dim,
+                              double* coords, int init_random, unsigned seed, int iterations);
+
 /* The reference's initial-coordinate stream: the first `count` values of
  * uniform_real_distribution<double>(-1,1) over mt19937(seed) (libstdc++). */
 int ge_uniform_stream(unsigned seed, long long count, double* out);

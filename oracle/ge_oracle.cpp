@@ -714,11 +714,191 @@ int orc_radius_step(int m, double* cA, double* rA, int dim, int coarse_is_base, 
 // ---------------------------------------------------------------------------
 // embed (src/embed.cpp:561-796): recursion unrolled from the coarsest level up.
 
-int orc_embed(int levels, const int* a_n, const int* a_off, const int* a_nz_off,
-              const int* a_ip, const int* a_ix, const double* a_dx, const int* p_rows,
-              const int* p_off, const int* p_nz_off, const int* p_ip, const int* p_ix,
-              int dim, unsigned seed, int base_iterations, int ml_iterations,
-              double* coords_out, int nthreads) {
+// ---------------------------------------------------------------------------
+// embedViaMinimization (src/embed.cpp:341-559), restated serially with the
+// reference's vector-of-vectors layout and loop order.
+
+int orc_embed_via_minimization(int n, const int* I, const int* J, int d, double* coords,
+                               int init_random, unsigned seed, int ITER) {
+  const double inf = std::numeric_limits<double>::infinity();
+  const double epsilon = 10e-12;
+  std::vector<std::vector<double>> X(n, std::vector<double>(d));
+  if (init_random) {
+    std::mt19937 gen(seed);
+    std::uniform_real_distribution<double> random(-1.0, 1.0);
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < d; k++) X[i][k] = random(gen);
+  } else {
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < d; k++) X[i][k] = coords[(size_t)i * d + k];
+  }
+  std::vector<std::vector<double>> dirs;
+  for (int k = 0; k < d; k++) {  // :363-379 (the d = 2, 3 literals list the same order)
+    std::vector<double> e(d, 0.0);
+    e[k] = 1;
+    dirs.push_back(e);
+    e[k] = -1;
+    dirs.push_back(e);
+  }
+  for (int iter = 0; iter < ITER; iter++) {
+    for (int i = 0; i < n; i++) {
+      std::vector<double>& x_i = X[i];
+      int count = 0;
+      for (int kk = I[i]; kk < I[i + 1]; kk++)
+        if (J[kk] != i) count++;
+      if (count == 0) continue;
+      double min_J_loc = inf;
+      double min_t = 0.0f;
+      double min_s = -1;
+      const double w = 1000000.0;
+      for (int s = 0; s < (int)dirs.size(); s++) {
+        const std::vector<double>& x_s = dirs[s];
+        double t = 0.5;
+        double jump = 0.25;
+        do {
+          double dJ_loc_dt = 0.0;
+          for (int r = 0; r < n; r++) {
+            if (i == r) continue;
+            const std::vector<double>& x_r = X[r];
+            double term1 = 0.0;
+            double term2 = 0.0;
+            for (int k = 0; k < d; k++) {
+              double u_k = x_s[k] - x_i[k];
+              double v_k = x_i[k] - x_r[k];
+              double z_k = (u_k * t + v_k);
+              term1 = term1 + z_k * z_k;
+              term2 = term2 + z_k * u_k;
+            }
+            if (term1 < epsilon) term1 = epsilon;
+            dJ_loc_dt += -((1.0 / sqrt(term1 * term1 * term1)) * term2);
+          }
+          for (int kk = I[i]; kk < I[i + 1]; kk++) {
+            int r = J[kk];
+            if (i == r) continue;
+            const std::vector<double>& x_r = X[r];
+            double term = 0.0;
+            for (int k = 0; k < d; k++) {
+              double a = (1 - t) * x_i[k] + t * x_s[k] - x_r[k];
+              term += w * 2.0 * a * (x_s[k] - x_i[k]);
+            }
+            dJ_loc_dt += term;
+          }
+          if (dJ_loc_dt < 0.0) t = t + jump;
+          else t = t - jump;
+          jump = jump / 2.0;
+        } while (jump > 1.e-4);
+        double J_loc = 0.0;
+        for (int r = 0; r < n; r++) {
+          if (i == r) continue;
+          const std::vector<double>& x_r = X[r];
+          double term1 = 0.0;
+          for (int k = 0; k < d; k++) {
+            double u_k = x_s[k] - x_i[k];
+            double v_k = x_i[k] - x_r[k];
+            double z_k = (u_k * t + v_k);
+            term1 = term1 + z_k * z_k;
+          }
+          if (term1 < epsilon) term1 = epsilon;
+          J_loc = J_loc + 1.0 / sqrt(term1);
+        }
+        for (int kk = I[i]; kk < I[i + 1]; kk++) {
+          int r = J[kk];
+          if (i == r) continue;
+          const std::vector<double>& x_r = X[r];
+          double term = 0.0;
+          for (int k = 0; k < d; k++) {
+            double a = (1 - t) * x_i[k] + t * x_s[k] - x_r[k];
+            term += a * a;
+          }
+          J_loc += w * term;
+        }
+        if (J_loc < min_J_loc) {
+          min_J_loc = J_loc;
+          min_t = t;
+          min_s = s;
+        }
+      }
+      if (min_s >= 0)
+        for (int k = 0; k < d; k++)
+          X[i][k] = X[i][k] * (1 - min_t) + dirs[(int)min_s][k] * min_t;
+    }
+  }
+  if (n > 1) {
+    std::vector<double> avg(d);
+    for (int i = 1; i < n; i++)
+      for (int k = 0; k < d; k++) avg[k] = avg[k] + X[i][k];
+    for (int k = 0; k < d; k++) avg[k] = avg[k] / (n - 1);
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < d; k++) X[i][k] -= avg[k];
+    double max_length = 0.0;
+    for (int i = 1; i < n; i++) {
+      double sum = 0.0;
+      for (int k = 0; k < d; k++) sum += X[i][k] * X[i][k];
+      double length = sqrt(sum);
+      if (max_length < length) max_length = length;
+    }
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < d; k++) X[i][k] = X[i][k] / max_length;
+  }
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < d; k++) coords[(size_t)i * d + k] = X[i][k];
+  return 0;
+}
+
+namespace {
+
+// anyToMultilevel(minimizer) applied to one level (src/embed.cpp:23-83): per
+// aggregate a, the members' internal edges as an r x r matrix of counts (the
+// CooMatrix of 1.0 entries summed by ToSparse), the minimizer on it, then the
+// result normalised by its largest norm and placed in a's ball.
+void any_to_multilevel_minimization(int n, const int* I, const int* J, int m, const int* PI,
+                                    const int* PJ, const int* v_A, const double* cA,
+                                    const double* rA, double* coords, int d, unsigned seed,
+                                    int min_iterations) {
+  (void)n;
+  for (int a = 0; a < m; a++) {
+    std::vector<int> v(PJ + PI[a], PJ + PI[a + 1]);
+    const int r = (int)v.size();
+    std::vector<std::map<int, double>> rows(r);
+    for (int i = 0; i < r; i++)
+      for (int k2 = I[v[i]]; k2 < I[v[i] + 1]; k2++) {
+        const int j = J[k2];
+        if (v_A[j] == a) {
+          int jp = -1;
+          for (int j2 = 0; j2 < r; j2++)
+            if (j == v[j2]) jp = j2;
+          rows[i][jp] += 1.0;
+        }
+      }
+    std::vector<int> ci(r + 1, 0), cj;
+    for (int i = 0; i < r; i++) {
+      for (const auto& e : rows[i]) cj.push_back(e.first);
+      ci[i + 1] = (int)cj.size();
+    }
+    // embedViaMinimization(A, d) starts from r x d zeros (:341-345), so it never
+    // draws: the empty-coords branch (:353) is not taken
+    std::vector<double> nc((size_t)r * d, 0.0);
+    orc_embed_via_minimization(r, ci.data(), cj.data(), d, nc.data(), 0, seed, min_iterations);
+    double mx = 0.0;
+    for (int i = 0; i < r; i++) {
+      double sum = 0.0;
+      for (int k = 0; k < d; k++) sum += nc[(size_t)i * d + k] * nc[(size_t)i * d + k];
+      const double mag = sqrt(sum);
+      if (mag > mx) mx = mag;
+    }
+    for (int i = 0; i < r; i++)
+      for (int k = 0; k < d; k++)
+        coords[(size_t)v[i] * d + k] = cA[(size_t)a * d + k] + rA[a] * (nc[(size_t)i * d + k] / mx);
+  }
+}
+
+}  // namespace
+
+static int embed_levels(int levels, const int* a_n, const int* a_off, const int* a_nz_off,
+                        const int* a_ip, const int* a_ix, const double* a_dx, const int* p_rows,
+                        const int* p_off, const int* p_nz_off, const int* p_ip, const int* p_ix,
+                        int dim, unsigned seed, int base_iterations, int ml_iterations,
+                        int min_iterations, double* coords_out, int nthreads) {
   for (int l = 0; l < levels; ++l)  // shape asserts (:564-570)
     if (p_rows[l] != a_n[l + 1]) return 2;
   orc_fa_params p;
@@ -750,6 +930,15 @@ int orc_embed(int levels, const int* a_n, const int* a_off, const int* a_nz_off,
     for (int a = 0; a < m; ++a)
       for (int c = P_ip(l)[a]; c < P_ip(l)[a + 1]; ++c) vA[P_ix(l)[c]] = a;
     std::vector<double> fine((size_t)a_n[l] * dim, 0.0);
+    if (l == 0 && min_iterations >= 0) {  // embedVia: the finest level's embedder
+      any_to_multilevel_minimization(a_n[l], A_ip(l), A_ix(l), m, P_ip(l), P_ix(l), vA.data(),
+                                     coarse.data(), rA.data(), fine.data(), dim, seed,
+                                     min_iterations);
+      cAc = std::move(coarse);
+      r_coarse = std::move(rA);
+      coarse = std::move(fine);
+      continue;
+    }
     rc = orc_force_atlas_ml(a_n[l], A_ip(l), A_ix(l), A_dx(l), m, P_ip(l), P_ix(l), vA.data(),
                             coarse.data(), rA.data(), fine.data(), dim, ml_iterations, seed,
                             &p, nthreads);
@@ -760,6 +949,28 @@ int orc_embed(int levels, const int* a_n, const int* a_off, const int* a_nz_off,
   }
   std::memcpy(coords_out, coarse.data(), sizeof(double) * coarse.size());
   return 0;
+}
+
+int orc_embed(int levels, const int* a_n, const int* a_off, const int* a_nz_off,
+              const int* a_ip, const int* a_ix, const double* a_dx, const int* p_rows,
+              const int* p_off, const int* p_nz_off, const int* p_ip, const int* p_ix,
+              int dim, unsigned seed, int base_iterations, int ml_iterations,
+              double* coords_out, int nthreads) {
+  return embed_levels(levels, a_n, a_off, a_nz_off, a_ip, a_ix, a_dx, p_rows, p_off, p_nz_off,
+                      p_ip, p_ix, dim, seed, base_iterations, ml_iterations, -1, coords_out,
+                      nthreads);
+}
+
+int orc_embed_via_minimization_ml(int levels, const int* a_n, const int* a_off,
+                                  const int* a_nz_off, const int* a_ip, const int* a_ix,
+                                  const double* a_dx, const int* p_rows, const int* p_off,
+                                  const int* p_nz_off, const int* p_ip, const int* p_ix,
+                                  int dim, unsigned seed, int base_iterations, int ml_iterations,
+                                  int min_iterations, double* coords_out, int nthreads) {
+  if (levels < 1 || min_iterations < 0) return 2;
+  return embed_levels(levels, a_n, a_off, a_nz_off, a_ip, a_ix, a_dx, p_rows, p_off, p_nz_off,
+                      p_ip, p_ix, dim, seed, base_iterations, ml_iterations, min_iterations,
+                      coords_out, nthreads);
 }
 
 }  // extern "C"

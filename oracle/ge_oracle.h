@@ -124,6 +124,23 @@ int orc_radius_step(int m, double* coords_A, double* r_A, int dim, int coarse_is
                     const double* coords_Ac, const double* r_Ac,
                     const int* ac_indptr, const int* ac_indices);
 
+/* embedViaMinimization (src/embed.cpp:341-559): coords n*dim in/out; init_random
+ * != 0 draws U(-1,1) from mt19937(seed) first (the empty-coords branch, :353-361). */
+int orc_embed_via_minimization(int n, const int* indptr, const int* indices, int dim,
+                               double* coords, int init_random, unsigned seed, int iterations);
+
+/* embedVia(As, P_Ts, d, anyToMultilevel(minimizer)) (src/embed.cpp:23-106,
+ * :108-338) with minimizer(A, d) = embedViaMinimization(A, d) (:341-345: r x d
+ * zeros, min_iterations sweeps; the reference uses 1000): the levels >= 1 are
+ * embedMultilevel (forceAtlas, radius steps, forceAtlasMultilevel), level 0 is
+ * the radius step then the per-aggregate minimizer.  levels >= 1. */
+int orc_embed_via_minimization_ml(int levels, const int* a_n, const int* a_off,
+                                  const int* a_nz_off, const int* a_indptr, const int* a_indices,
+                                  const double* a_data, const int* p_rows, const int* p_off,
+                                  const int* p_nz_off, const int* p_indptr, const int* p_indices,
+                                  int dim, unsigned seed, int base_iterations, int ml_iterations,
+                                  int min_iterations, double* coords_out, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

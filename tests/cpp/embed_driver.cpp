@@ -3,10 +3,13 @@
 // embed(As, hierarchy, d).  The input CSR comes from a small binary file (the
 // reference reads it with linalgcpp parsers, examples/embed.cpp:80-91); the
 // coordinates go to a binary file for the test to compare.
-//   embed_driver <in.bin> <out.bin> <dim> <seed> [multilevel]
+//   embed_driver <in.bin> <out.bin> <dim> <seed> [ml | via]
+// "via": embedVia(As, hierarchy, d, anyToMultilevel(embedViaMinimization)), the
+// reference's alternative multilevel embedder (src/embed.cpp:23-338).
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <string>
 #include <vector>
 
 #include "embed.hpp"
@@ -42,7 +45,12 @@ int main(int argc, char** argv) {
     As.push_back(dev);
   }
   std::vector<std::vector<double>> coords;
-  if (argc > 5) {
+  if (argc > 5 && std::string(argv[5]) == "via") {
+    using Embedder = std::vector<std::vector<double>> (*)(const SparseMatrix&, const int);
+    coords = partition::embedVia(
+        As, hierarchy, dim,
+        partition::anyToMultilevel(static_cast<Embedder>(partition::embedViaMinimization)));
+  } else if (argc > 5) {
     std::vector<double> r_A;
     std::vector<std::vector<double>> coords_A;
     coords = partition::embedMultilevel(As, hierarchy, dim, 0, r_A, coords_A);

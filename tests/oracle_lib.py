@@ -79,6 +79,12 @@ def lib():
         L.orc_embed.argtypes = [ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _i32p, _f64p,
                                 _i32p, _i32p, _i32p, _i32p, _i32p, ctypes.c_int, ctypes.c_uint,
                                 ctypes.c_int, ctypes.c_int, _f64p, ctypes.c_int]
+        L.orc_embed_via_minimization.argtypes = [ctypes.c_int, _i32p, _i32p, ctypes.c_int, _f64p,
+                                                 ctypes.c_int, ctypes.c_uint, ctypes.c_int]
+        L.orc_embed_via_minimization_ml.argtypes = [
+            ctypes.c_int, _i32p, _i32p, _i32p, _i32p, _i32p, _f64p, _i32p, _i32p, _i32p, _i32p,
+            _i32p, ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f64p,
+            ctypes.c_int]
         L.orc_radius_step.argtypes = [ctypes.c_int, _f64p, _f64p, ctypes.c_int, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, _i32p, _i32p]
@@ -270,6 +276,28 @@ def _concat_levels(As, hier):
     p_ip = np.concatenate([p[0] for p in hier] + [np.zeros(1)]).astype(np.int32)
     p_ix = np.concatenate([p[1] for p in hier] + [np.zeros(1)]).astype(np.int32)
     return a_n, a_off, a_nz, a_ip, a_ix, a_dx, p_rows, p_off, p_nz, p_ip, p_ix
+
+
+def embed_via_minimization(A, dim, coords=None, iterations=10, seed=0):
+    ip, ix, _ = _csr(A)
+    n = len(ip) - 1
+    X = np.zeros((n, dim)) if coords is None else np.array(coords, dtype=np.float64)
+    X = np.ascontiguousarray(X)
+    rc = lib().orc_embed_via_minimization(n, ip, ix, dim, X.reshape(-1), int(coords is None),
+                                          seed, iterations)
+    assert rc == 0, rc
+    return X
+
+
+def embed_via_minimization_ml(As, hier, dim, seed=0, base_iterations=100000, ml_iterations=100,
+                              min_iterations=1000, nthreads=0):
+    parts = _concat_levels(As, hier)
+    out = np.empty((len(As[0][0]) - 1, dim))
+    rc = lib().orc_embed_via_minimization_ml(len(hier), *parts, dim, seed, base_iterations,
+                                             ml_iterations, min_iterations, out.reshape(-1),
+                                             nthreads)
+    assert rc == 0, rc
+    return out
 
 
 def embed(As, hier, dim, seed=0, base_iterations=100000, ml_iterations=100, nthreads=0):

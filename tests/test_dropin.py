@@ -50,6 +50,29 @@ def test_dropin_driver_c1(tmp_path, golden, multilevel_api):
     assert np.array_equal(X, g["coords"])
 
 
+@pytest.mark.gpu
+def test_dropin_embed_via_minimization(tmp_path, golden, oracle):
+    """embedVia(As, P_Ts, 2, anyToMultilevel(embedViaMinimization)) through the
+    drop-in headers (coarser levels on the device, the finest level's
+    per-aggregate minimizer in libge) against the oracle's restatement of
+    src/embed.cpp:23-559 on config 1."""
+    g = golden("embed_c1_er1000_d2")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    exe = build_driver(tmp_path)
+    inp, out = str(tmp_path / "a.bin"), str(tmp_path / "x.bin")
+    write_csr(inp, A)
+    seed = int(g["seed"])
+    r = subprocess.run([exe, inp, out, "2", str(seed), "via"], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stderr
+    X = np.fromfile(out, dtype=np.float64).reshape(-1, 2)
+    hier = oracle.partition(A, 0.1)
+    As = oracle.hierarchy_As(A, hier)
+    want = oracle.embed_via_minimization_ml(As, hier, 2, seed=seed, base_iterations=100000,
+                                            ml_iterations=100, min_iterations=1000)
+    assert np.array_equal(X, want)
+
+
 def _read_csrs(path, count):
     buf = open(path, "rb").read()
     off, out = 0, []

@@ -151,3 +151,22 @@ def test_device_entry_points_fail_loudly_without_gpu():
         pass
     with pytest.raises(ge.GeError):
         ge.Context(0)
+
+
+@pytest.mark.parametrize("dim,init", [(2, True), (3, True), (4, False), (3, False)])
+def test_embed_via_minimization(oracle, dim, init):
+    """ge_embed_via_minimization (host C++, directions on OpenMP threads) against
+    the oracle's serial restatement of src/embed.cpp:341-559, bit for bit; n > 64
+    takes the threaded path."""
+    for n in (1, 2, 12, 90):
+        if n == 1:
+            A = (np.array([0, 0], np.int32), np.zeros(0, np.int32), np.zeros(0))
+        elif n == 2:
+            A = (np.array([0, 1, 2], np.int32), np.array([1, 0], np.int32), np.ones(2))
+        else:
+            A = G.largest_component(G.rmat(n, 4 * n, seed=n))
+        m = len(A[0]) - 1
+        X0 = None if init else G.random_coords(m, dim, seed=3)
+        got = ge.embed_via_minimization(A, dim, coords=X0, iterations=6, seed=17)
+        want = oracle.embed_via_minimization(A, dim, coords=X0, iterations=6, seed=17)
+        assert np.array_equal(got, want, equal_nan=True), n
