@@ -70,7 +70,10 @@ def test_dropin_embed_via_minimization(tmp_path, golden, oracle):
     As = oracle.hierarchy_As(A, hier)
     want = oracle.embed_via_minimization_ml(As, hier, 2, seed=seed, base_iterations=100000,
                                             ml_iterations=100, min_iterations=1000)
-    assert np.array_equal(X, want)
+    # a one-member aggregate has no edges: the minimizer leaves it at 0, its largest
+    # norm is 0 and the reference places it at c_a + r_a * (0 / 0) = NaN
+    bad = ~((X == want) | (np.isnan(X) & np.isnan(want)))
+    assert not bad.any(), (int(bad.sum()), np.argwhere(bad)[:5], X[bad][:5], want[bad][:5])
 
 
 def _read_csrs(path, count):
