@@ -1,4 +1,4 @@
-"""Device parity at the BASELINE configs' own sizes (configs[1], [2], [4]) plus the
+"""Device parity at the BASELINE configs' own sizes (configs[1] to [4]) plus the
 reference options the small-graph suites do not cover.
 
 The dynamics are chaotic and every kernel is strict fp64 in the reference's op
@@ -78,6 +78,38 @@ def test_c3_level0_sampled_aggregates(ctx, oracle):
     want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=100, seed=5)
     rows = np.concatenate([PT[1][PT[0][a]:PT[0][a + 1]] for a in aggs])
     assert len(big) == 4 and sizes[aggs].max() > 2000
+    assert np.array_equal(got[rows], want[rows])
+    assert np.isfinite(got).all()
+
+
+def test_c4_level0_sampled_aggregates(ctx, oracle):
+    """configs[3] (C4, the headline): the 10M-id R-MAT LCC (n = 4.39M), device
+    partition, level-0 forceAtlasMultilevel (2 iterations: the symmetric streamed
+    kernel with its sweep hand-overs at full size) against the oracle on the largest
+    aggregate (41 930 members), aggregates around the streamed / resident split and
+    random small ones."""
+    import time
+    t0 = time.perf_counter()
+    L = ge.largest_component(ge.rmat_csr(10_000_000, 80_000_000, seed=12345))
+    _progress(t0, f"C4 LCC n={len(L[0]) - 1}")
+    PT = ctx.partition(L, 0.125)[0]
+    _progress(t0, "C4 device partition")
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = ge.uniform_stream(7, m * 3).reshape(m, 3)
+    rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
+    got = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=2, seed=5)
+    _progress(t0, "C4 device level done")
+    sizes = np.diff(PT[0])
+    order = np.argsort(sizes, kind="stable")
+    big = [int(order[-1])] + [a for a in order if 2000 < sizes[a] <= 4000][:3]
+    split = [a for a in order if 200 <= sizes[a] <= 2000][-4:]
+    small = np.random.default_rng(4).choice(np.nonzero(sizes <= 200)[0], 100, replace=False)
+    aggs = np.array(sorted(set(big) | set(split) | set(small.tolist())), dtype=np.int32)
+    want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
+    _progress(t0, "C4 oracle aggregates done")
+    rows = np.concatenate([PT[1][PT[0][a]:PT[0][a + 1]] for a in aggs])
+    assert sizes[aggs].max() > 40000
     assert np.array_equal(got[rows], want[rows])
     assert np.isfinite(got).all()
 
