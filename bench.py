@@ -276,11 +276,13 @@ def run_multilevel(args, rank, world, local, dev):
     -> device P^T A P -> K forceAtlasMultilevel iterations of level 0."""
     import torch
     import ge_amd as ge
+    ctx = ge.Context(local)
     t0 = time.perf_counter()
-    L = ge.largest_component(ge.rmat_csr(args.n, args.draws, seed=args.seed))
+    # R-MAT + largest component on the device (csrc/ge_graph.hip; same arrays as the
+    # host generator, tests/test_gpu_graph.py)
+    L = ctx.rmat_csr(args.n, args.draws, seed=args.seed, lcc=True)
     t_gen = time.perf_counter() - t0
     n0, nnz0 = len(L[0]) - 1, len(L[1])
-    ctx = ge.Context(local)
     t0 = time.perf_counter()
     hier_full = ctx.partition(L, 0.125)
     t_part = time.perf_counter() - t0
@@ -392,7 +394,7 @@ def run_multilevel(args, rank, world, local, dev):
                                        "and credits both ordered pairs",
                      "avg_launch_ms": rep_ms, "launches": rep_launches},
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
-        "setup_seconds": {"graph_host": t_gen, "partition_device": t_part,
+        "setup_seconds": {"graph_device": t_gen, "partition_device": t_part,
                           "partition_host": t_part_host, "ptap_device": t_ptap},
     }
     for p in plans.values():
@@ -420,8 +422,9 @@ def run_single_level(args, rank, world, local, dev):
     import torch
     import ge_amd as ge
     from ge_amd.dist import row_shards
+    ctx = ge.Context(local)
     t0 = time.perf_counter()
-    A = ge.rmat_csr(args.n, args.draws, seed=args.seed)
+    A = ctx.rmat_csr(args.n, args.draws, seed=args.seed)
     n, nnz = len(A[0]) - 1, len(A[1])
     X0 = ge.uniform_stream(args.seed, n * args.dim).reshape(n, args.dim)  # ref init order
     log(rank, f"R-MAT n={n} nnz={nnz} generated in {time.perf_counter() - t0:.1f}s")
@@ -432,7 +435,6 @@ def run_single_level(args, rank, world, local, dev):
     xa = torch.zeros((npad, args.dim), dtype=torch.float64, device=dev)
     xa[:n] = torch.from_numpy(X0).to(dev)
     xb = torch.zeros_like(xa)
-    ctx = ge.Context(local)
     work = torch.cuda.Stream(dev)
     torch.cuda.set_stream(work)
     ctx.set_stream(work.cuda_stream)

@@ -120,6 +120,10 @@ _SIGS = {
                                              _vp, _ip]),
     "ge_embed_via_minimization": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, ctypes.c_int, _f64p,
                                                  ctypes.c_int, ctypes.c_uint, ctypes.c_int]),
+    "ge_rmat_csr_device": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                          ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ge_largest_component_device": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p,
+                                                   ctypes.POINTER(_vp)]),
     # multi-GPU (ge_dist.hip)
     "ge_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "ge_comm_create": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
@@ -320,6 +324,19 @@ class Context:
             ptr(None if Ac is None else Ac[0], np.int32),
             ptr(None if Ac is None else Ac[1], np.int32), ctypes.byref(used)))
         return rA, cA.reshape(m, dim), bool(used.value)
+
+    def rmat_csr(self, n, draws, seed=12345, lcc=False):
+        """ge_rmat_csr_device: the R-MAT (or its largest component) built on the device."""
+        h = _vp()
+        _check(lib().ge_rmat_csr_device(self.h, n, draws, seed, int(lcc), ctypes.byref(h)))
+        return _take_csr(h)
+
+    def largest_component(self, A):
+        ip, ix, dx = _csr(A)
+        h = _vp()
+        _check(lib().ge_largest_component_device(self.h, len(ip) - 1, ip, ix, dx,
+                                                 ctypes.byref(h)))
+        return _take_csr(h)
 
     def selftest_math(self, samples=1 << 24, seed=1):
         bad = ctypes.c_longlong()

@@ -321,6 +321,14 @@ int ge_selftest_math(ge_ctx* ctx, long long samples, unsigned long long seed,
 int ge_rmat_csr(int n, long long draws, unsigned long long seed, ge_csr** out);
 int ge_largest_component(int n, const int* indptr, const int* indices, const double* data,
                          ge_csr** out);
+/* The same two on the device (graph-embed_amd/csrc/ge_graph.hip), same results:
+ * R-MAT by counter-based generation + radix sort + compaction, lcc != 0 returns
+ * its largest connected component (hooking + pointer jumping, vertices renumbered
+ * in ascending original id, examples/embedder.cpp:35-93). */
+int ge_rmat_csr_device(ge_ctx* ctx, int n, long long draws, unsigned long long seed, int lcc,
+                       ge_csr** out);
+int ge_largest_component_device(ge_ctx* ctx, int n, const int* indptr, const int* indices,
+                                const double* data, ge_csr** out);
 
 #ifdef __cplusplus
 }
