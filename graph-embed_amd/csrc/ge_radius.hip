@@ -156,7 +156,9 @@ __global__ void pop_kernel(int nl, int round, const int* __restrict__ live,
   const double t = et[e];
   const u64 o = time_ord(t);
   const u64 ij = ((u64)(unsigned)i << 32) | (unsigned)j;
-  const bool li = r[i] <= 0.0, lj = r[j] <= 0.0;
+  // liveness as of the round's start: best_t is set exactly for the live endpoints
+  // (r[] itself is being written by this kernel's other pops)
+  const bool li = best_t[i] != 0, lj = best_t[j] != 0;
   const bool ready = (!li || (best_t[i] == o && best_ij[i] == ij)) &&
                      (!lj || (best_t[j] == o && best_ij[j] == ij));
   if (!ready) return;
