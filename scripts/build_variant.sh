@@ -16,6 +16,6 @@ done
 wait
 CPP_OBJ=$(for f in $HERE/csrc/*.cpp; do echo $HERE/build/$(basename $f .cpp).o; done)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libge.so $OUT/*.o $CPP_OBJ \
-  $(g++ -print-file-name=libgomp.so) -Wl,-soname,libge.so
+  $(g++ -print-file-name=libgomp.so) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libge.so
 rm -f $OUT/*.o
 echo $OUT/libge.so
