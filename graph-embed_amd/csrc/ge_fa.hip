@@ -411,7 +411,6 @@ struct FaRows {
 
 constexpr int kSmallMax = 512;  // one row group per thread group below
 constexpr int kSmallDefault = 64;
-constexpr int kSmallT = 512;
 constexpr int kSmallNnz = 6144;
 // CSR entries staged in LDS (the 4-D double-buffered term tile leaves less room)
 constexpr int small_nnz_cap(int D) { return D == 4 ? 4096 : kSmallNnz; }

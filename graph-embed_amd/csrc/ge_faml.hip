@@ -868,19 +868,20 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     struct Unit { int a, A, pb, T, kind; double est; };
     std::vector<Unit> us;
     int pb = 0;
-    double est_max = 0.0;
     for (size_t b = 0; b < big.size(); ++b) {
       if (rows_mode[b]) continue;
       for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], 0, 2.0 * A});
-      est_max = std::max(est_max, 2.0 * (T[b] - 1));
       pb += T[b];
     }
     std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b)
       if (rows_mode[b])
         for (int A = 0; A < T[b]; ++A) rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
-    for (size_t k = 0; k < rows_units.size(); ++k) {  // spread among the sweeps
-      rows_units[k].est = est_max * (double)k / (double)std::max<size_t>(rows_units.size(), 1);
+    // row blocks have no dependencies and each spans its aggregate's whole width:
+    // first in the queue (measured on per-rank shares of C4: N = 4 69 ms per
+    // iteration against 80 ms when spread among the sweeps, N = 2 unchanged)
+    for (size_t k = 0; k < rows_units.size(); ++k) {
+      rows_units[k].est = -1.0;
       us.push_back(rows_units[k]);
     }
     std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {

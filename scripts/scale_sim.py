@@ -1,0 +1,58 @@
+"""Multi-GPU rehearsal on one GPU for the C4 multilevel level: for N = 1, 2, 4, 8
+every rank's share (ge_assign_aggregates, the deal bench.py uses) runs as its own
+subset plan, one after another, and its kernel time per iteration is measured.
+max over ranks approximates the N-GPU step (the member all-gather, once per call,
+is left out); efficiency = t(1) / (N * max).  Prints one JSON line per N."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "graph-embed_amd", "py"))
+import ge_amd as ge  # noqa: E402
+
+
+def main():
+    n, draws, dim, iters = 10_000_000, 80_000_000, 3, int(os.environ.get("ITERS", "5"))
+    ctx = ge.Context(0)
+    L = ctx.rmat_csr(n, draws, seed=12345, lcc=True)
+    PT = ctx.partition(L, 0.125)[0]
+    m = PT[2]
+    n0 = len(L[0]) - 1
+    vA = ge.vertex_of(PT)
+    dev = torch.device("cuda:0")
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d = dict(ip=T(L[0]), ix=T(L[1]), dx=T(L[2]), pip=T(PT[0]), pix=T(PT[1]), vA=T(vA),
+             cA=T(ge.uniform_stream(7, m * dim)), rA=T(0.01 + 0.19 * (ge.uniform_stream(8, m) + 1) / 2),
+             init=T(ge.uniform_stream(5, n0 * dim)))
+    X = torch.zeros((n0, dim), dtype=torch.float64, device=dev)
+    t1 = None
+    for N in (1, 2, 4, 8):
+        owner = ge.assign_aggregates(PT, L[0], N)
+        times = []
+        for r in range(N):
+            mine = np.flatnonzero(owner == r).astype(np.int32)
+            p = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
+                            PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
+                            dim, iterations=iters, aggs=mine if N > 1 else None)
+            p.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            ctx.sync()
+            p.set_profiling(True)
+            t0 = time.perf_counter()
+            p.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
+            ctx.sync()
+            times.append((time.perf_counter() - t0) / iters * 1e3)
+            rep_ms, _, _ = p.repulse_ms()
+            p.close()
+        t1 = t1 or times[0]
+        print(json.dumps({"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times),
+                          "efficiency": t1 / (N * max(times))}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
