@@ -318,20 +318,28 @@ constexpr int kBigDefaultR = 1, kBigDefaultU = 1;
 
 template <int D>
 __global__ void __launch_bounds__(kHT)
-faml_huge_init(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ix,
-               const int* __restrict__ vA, const int* __restrict__ ip,
-               const int* __restrict__ ix, const double* __restrict__ dx,
-               const double* __restrict__ init, double* __restrict__ Xp,
-               double* __restrict__ DP, double* __restrict__ Fprev, int use_weights) {
+faml_huge_init(int nrows, const int* __restrict__ rows, const double* __restrict__ init,
+               double* __restrict__ Xp, double* __restrict__ Fprev) {
   const int q = blockIdx.x * kHT + threadIdx.x;
   if (q >= nrows) return;
   const int c = rows[q];
-  const int v = pt_ix[c];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     Xp[(size_t)c * D + k] = init[(size_t)c * D + k];
     Fprev[(size_t)c * D + k] = 0.0;
   }
+}
+
+// internal deg + 1 of the streamed members (:362-383): a property of the graph
+// and P_T, computed once per plan (a hub row's serial sum takes tens of ms).
+__global__ void __launch_bounds__(kHT)
+faml_huge_dp(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ix,
+             const int* __restrict__ vA, const int* __restrict__ ip, const int* __restrict__ ix,
+             const double* __restrict__ dx, double* __restrict__ DP, int use_weights) {
+  const int q = blockIdx.x * kHT + threadIdx.x;
+  if (q >= nrows) return;
+  const int c = rows[q];
+  const int v = pt_ix[c];
   DP[c] = internal_dp1(v, vA[v], ip, ix, dx, vA, use_weights);
 }
 
@@ -943,10 +951,14 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   }
   hipLaunchKernelGGL(pos_of_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, pl->pt_ix,
                      pl->pos.p);
-  if (pl->nrows > 0)
+  if (pl->nrows > 0) {
     hipLaunchKernelGGL(edge_code_kernel, dim3((pl->nrows + 255) / 256), dim3(256), 0, st,
                        pl->nrows, pl->rows.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip,
                        pl->ix, pl->ecode.p);
+    hipLaunchKernelGGL(faml_huge_dp, dim3((pl->nrows + kHT - 1) / kHT), dim3(kHT), 0, st,
+                       pl->nrows, pl->rows.p, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, pl->DP.p,
+                       pl->c.use_weights);
+  }
   GE_HIP(hipGetLastError());
   for (int k = 0; k < 3; ++k) {
     GE_HIP(hipStreamCreateWithFlags(&pl->side[k], hipStreamNonBlocking));
@@ -983,8 +995,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     if (pl->nrows > 0) {
       const int nr = pl->nrows;
       hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
-                         nr, pl->rows.p, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, init,
-                         pl->Xa.p, pl->DP.p, pl->Fprev.p, c.use_weights);
+                         nr, pl->rows.p, init, pl->Xa.p, pl->Fprev.p);
       GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
