@@ -60,5 +60,6 @@ int main(int argc, char** argv) {
   std::ofstream out(argv[2], std::ios::binary);
   for (const auto& row : coords) out.write((const char*)row.data(), sizeof(double) * dim);
   partition::writeCoords(coords, std::string(argv[2]) + ".txt");
+  partition::writeCoordsExact(coords, std::string(argv[2]) + ".exact.txt");
   return 0;
 }

@@ -48,6 +48,10 @@ def test_dropin_driver_c1(tmp_path, golden, multilevel_api):
     assert "embedding layer" in r.stdout  # the reference's progress lines
     X = np.fromfile(out, dtype=np.float64).reshape(-1, 2)
     assert np.array_equal(X, g["coords"])
+    # the reference's text format (6 significant digits) and the exact extension
+    txt = np.loadtxt(out + ".txt")
+    assert np.allclose(txt, X, rtol=1e-5, atol=0)
+    assert np.array_equal(np.loadtxt(out + ".exact.txt"), X)
 
 
 @pytest.mark.gpu
