@@ -253,7 +253,11 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const int base = pt_ip[u.x];
     const int s = pt_ip[u.x + 1] - base;
     if (u.w) {
+      // a row block spans its aggregate's whole width: the launch's critical path
+      // when the aggregate is large, so its wave takes issue priority on the SIMD
+      __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
+      __builtin_amdgcn_s_setprio(0);
       continue;
     }
     int* tprog = prog + u.z + A;  // tprog[t]: column tile A + t
