@@ -863,15 +863,34 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::iota(by_T.begin(), by_T.end(), 0);
     std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
     std::vector<char> rows_mode(big.size(), 0);
-    double work = 0.0;
-    for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
-    double chain_k = 2.5;
+    // Choose how many of the largest aggregates run as row blocks: the launch
+    // lasts about max(work / waves, the longest sweep chain ~chain_k T, the
+    // longest row block ~row_k T) tile-times, where a sweep aggregate costs
+    // T^2 / 2 + T sweep-tiles and a row-block aggregate 0.8 T^2 (every ordered
+    // pair; its waves run at raised priority).  Take the count that minimises it.
+    double chain_k = 2.5, row_k = 0.8;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
-    for (size_t r = 0; r < by_T.size() && chain_k > 0.0; ++r) {
-      const size_t b = by_T[r];
-      if (chain_k * T[b] <= work / waves) break;
-      rows_mode[b] = 1;
-      work += 0.8 * T[b] * (double)T[b] - (0.5 * T[b] * (double)T[b] + T[b]);
+    if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
+    if (chain_k > 0.0) {
+      double work = 0.0;
+      for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
+      double best = 1e300;
+      size_t best_k = 0;
+      for (size_t k = 0; k <= by_T.size(); ++k) {  // the k largest as row blocks
+        const double sweep_chain = k < by_T.size() ? chain_k * T[by_T[k]] : 0.0;
+        const double row_path = k > 0 ? row_k * T[by_T[0]] : 0.0;
+        const double pred = std::max(work / waves, std::max(sweep_chain, row_path));
+        if (pred < best * 0.999) {
+          best = pred;
+          best_k = k;
+        }
+        if (k < by_T.size()) {
+          const double t = T[by_T[k]];
+          work += 0.8 * t * t - (0.5 * t * t + t);
+        }
+        if (sweep_chain <= work / waves && k > 0) break;  // further switches only add work
+      }
+      for (size_t k = 0; k < best_k; ++k) rows_mode[by_T[k]] = 1;
     }
     struct Unit { int a, A, pb, T, kind; double est; };
     std::vector<Unit> us;
