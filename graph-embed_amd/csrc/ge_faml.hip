@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <numeric>
 #include <vector>
@@ -864,33 +865,53 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
     std::vector<char> rows_mode(big.size(), 0);
     // Choose how many of the largest aggregates run as row blocks: the launch
-    // lasts about max(work / waves, the longest sweep chain ~chain_k T, the
-    // longest row block ~row_k T) tile-times, where a sweep aggregate costs
-    // T^2 / 2 + T sweep-tiles and a row-block aggregate 0.8 T^2 (every ordered
-    // pair; its waves run at raised priority).  Take the count that minimises it.
+    // lasts about max(work / waves, the longest row block ~row_k T, the start of
+    // the sweeps + the longest sweep chain ~chain_k T) tile-times, where a sweep
+    // aggregate costs T^2 / 2 + T sweep-tiles and a row-block aggregate 0.8 T^2
+    // (every ordered pair; its waves run at raised priority).  Row blocks are first
+    // in the queue, so when they hold most of the waves the sweeps start late and
+    // run slower than modelled beside the raised row waves: mixes whose row blocks
+    // exceed half the waves are not taken (measured on per-rank shares of C4,
+    // N = 4: 20 of 24 aggregates as row blocks 70 ms per iteration, 7 of 25 (4 090
+    // row blocks) 58 ms, all 52 ms).
+    // Take the count that minimises it.
     double chain_k = 2.5, row_k = 0.8;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
+    double best = 1e300;
+    size_t best_k = 0;
     if (chain_k > 0.0) {
-      double work = 0.0;
+      double work = 0.0, row_work = 0.0, row_units = 0.0;
       for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
-      double best = 1e300;
-      size_t best_k = 0;
       for (size_t k = 0; k <= by_T.size(); ++k) {  // the k largest as row blocks
-        const double sweep_chain = k < by_T.size() ? chain_k * T[by_T[k]] : 0.0;
+        const double start = row_units > waves ? row_work / waves : 0.0;
+        const double sweep_chain = k < by_T.size() ? start + chain_k * T[by_T[k]] : 0.0;
         const double row_path = k > 0 ? row_k * T[by_T[0]] : 0.0;
         const double pred = std::max(work / waves, std::max(sweep_chain, row_path));
-        if (pred < best * 0.999) {
+        const bool mixed_late = 2.0 * row_units > waves && k < by_T.size();
+        if (!mixed_late && pred < best * 0.999) {
           best = pred;
           best_k = k;
         }
         if (k < by_T.size()) {
           const double t = T[by_T[k]];
           work += 0.8 * t * t - (0.5 * t * t + t);
+          row_work += 0.8 * t * t;
+          row_units += t;
         }
-        if (sweep_chain <= work / waves && k > 0) break;  // further switches only add work
       }
       for (size_t k = 0; k < best_k; ++k) rows_mode[by_T[k]] = 1;
+      if (std::getenv("GE_FAML_PLAN_DEBUG"))
+        std::fprintf(stderr,
+                     "faml plan: %zu streamed aggregates, T max %d, waves %.0f, work/waves %.1f "
+                     "(all sweeps), %zu as row blocks, predicted %.1f tile-times\n",
+                     big.size(), T[by_T[0]], waves,
+                     [&] {
+                       double w = 0.0;
+                       for (int t : T) w += 0.5 * t * (double)t + t;
+                       return w / waves;
+                     }(),
+                     best_k, best);
     }
     struct Unit { int a, A, pb, T, kind; double est; };
     std::vector<Unit> us;

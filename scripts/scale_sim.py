@@ -31,9 +31,9 @@ def main():
              init=T(ge.uniform_stream(5, n0 * dim)))
     X = torch.zeros((n0, dim), dtype=torch.float64, device=dev)
     t1 = None
-    for N in (1, 2, 4, 8):
+    for N in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
         owner = ge.assign_aggregates(PT, L[0], N)
-        times = []
+        times, reps = [], []
         for r in range(N):
             mine = np.flatnonzero(owner == r).astype(np.int32)
             p = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
@@ -47,9 +47,10 @@ def main():
             ctx.sync()
             times.append((time.perf_counter() - t0) / iters * 1e3)
             rep_ms, _, _ = p.repulse_ms()
+            reps.append(rep_ms)
             p.close()
         t1 = t1 or times[0]
-        print(json.dumps({"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times),
+        print(json.dumps({"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times), "repulse_ms_by_rank": reps,
                           "efficiency": t1 / (N * max(times))}), flush=True)
     ctx.close()
 
