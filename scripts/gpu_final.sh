@@ -19,7 +19,7 @@ timeout -k 10 500 python bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?
 echo "bench rc=$rc"; cat $OUT/bench.json
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o c4 -- \
-  python3 bench.py --no-cpu-baseline > $OUT/trace.log 2>&1; rc=$?
+  python3 bench.py --no-cpu-baseline --no-end-to-end > $OUT/trace.log 2>&1; rc=$?
 echo "trace rc=$rc"
 cp $(find $OUT/trace -name "*kernel_stats.csv" | head -1) $OUT/rocprof_kernel_stats_c4.csv; rm -rf $OUT/trace
 [ $rc -eq 0 ] || exit $rc
