@@ -16,8 +16,11 @@ forceAtlasMultilevel call with iterations = K (random init, K iterations, ball
 mapping: src/embed.cpp:793 runs the same call with 100), strict fp64 (bit-exact
 with the reference's op order).  value = iterations/s of the whole job.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-every rank builds the same graph and hierarchy; the level's aggregates are dealt
+Multi-GPU: `bench.py --gpus N` starts N ranks itself (torch.distributed.run as a
+child process, before this process touches the GPU; one rank per GPU over RCCL),
+or runs as one of them under an outside launcher (python -m
+torch.distributed.run --nproc-per-node N bench.py --gpus N).  Every rank builds
+the same graph and hierarchy; the level's aggregates are dealt
 to ranks by cost (longest processing time first).  Aggregates exchange nothing
 during the iterations (:454, :462 read only the frozen coarse coordinates); one
 all-gather of the members' coordinates completes the call.  Total work is fixed:
@@ -74,6 +77,8 @@ def parse():
                     help="c3/c4: skip the timed partition::embed over the whole hierarchy")
     ap.add_argument("--partition-host", action="store_true",
                     help="c3/c4: also time the library's host partition (minutes at c4)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check the process group and exit (no GPU work)")
     return ap.parse_args()
 
 
@@ -113,15 +118,15 @@ def host_info():
 
 
 def baseline_threads():
-    """OpenMP threads for the CPU baseline: OMP_NUM_THREADS (the GPU box sets it to
-    its per-GPU CPU share) or else this process's CPU affinity."""
-    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if env:
-        return env
+    """OpenMP threads for the CPU baseline: the CPUs this process may run on (its
+    affinity), so a small CPU share is not oversubscribed; OMP_NUM_THREADS only
+    lowers it."""
     try:
-        return len(os.sched_getaffinity(0))
+        cpus = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        cpus = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(cpus, env) if env else cpus
 
 
 def baseline_record(value, unit, threads, sample, per_iter):
@@ -224,17 +229,36 @@ def cpu_baseline_ml(L, PT, vA, cA, rA, dim, seconds, rank):
     t, c, _ = run(stride)
     stride = max(1, int(stride * t / seconds)) if t > 0 else 1
     t, c, na = run(stride)
-    per_iter = t * cost.sum() / c
+    # cost units per second of one thread, then the whole level on `threads` threads:
+    # the reference deals whole aggregates to threads (`omp parallel for`,
+    # include/forceatlas.hpp:340), so an iteration lasts at least as long as its
+    # largest aggregate on one thread (the serial tail) and at least the total work
+    # spread over all threads -- the larger of the two (a list-scheduling lower
+    # bound, so the baseline is not understated)
+    rate = c / (t * threads)
+    spread = cost.sum() / (rate * threads)
+    tail = cost.max() / rate
+    per_iter = max(spread, tail)
     log(rank, f"cpu baseline (multilevel): stride {stride}, {t:.2f}s on {threads} threads "
-              f"-> {per_iter:.2f}s/iteration")
-    return baseline_record(1.0 / per_iter, "iterations/s", threads,
-                           f"oracle forceAtlasMultilevel, 1 iteration over every {stride}-th "
-                           f"aggregate of level 0 ({na} aggregates, {t:.1f}s, OpenMP {threads} "
-                           "threads), scaled by the pair+edge cost of the whole level", per_iter)
+              f"-> {per_iter:.2f}s/iteration (spread {spread:.2f}s, serial tail {tail:.2f}s)")
+    rec = baseline_record(1.0 / per_iter, "iterations/s", threads,
+                          f"oracle forceAtlasMultilevel, 1 iteration over every {stride}-th "
+                          f"aggregate of level 0 ({na} aggregates, {t:.1f}s, OpenMP {threads} "
+                          "threads); per-thread rate scaled to the whole level as max(total "
+                          "cost / threads, largest aggregate on one thread)", per_iter)
+    rec["model"] = {"spread_seconds": spread, "serial_tail_seconds": tail,
+                    "largest_aggregate": int(s.max()), "cost_units": "s(s-1) + CSR entries"}
+    if "extrapolated_all_physical_cores" in rec:  # the serial tail does not shrink
+        pc = rec["extrapolated_all_physical_cores"]["cores"]
+        rec["extrapolated_all_physical_cores"]["value"] = 1.0 / max(cost.sum() / (rate * pc), tail)
+        rec["extrapolated_all_physical_cores"]["note"] = ("per-thread rate on every physical "
+                                                          "core, serial tail kept; not measured")
+    return rec
 
 
 def timed(args, world, dev, fn):
-    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+    """W untimed steps, then K steps between barrier + synchronize.  Returns (max over
+    ranks, every rank's seconds)."""
     import torch
     import torch.distributed as dist
     fn(args.warmup, timed=False)
@@ -248,12 +272,14 @@ def timed(args, world, dev, fn):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
+    if world == 1:
+        return elapsed, [elapsed]
+    tdev = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+    every = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(every, t)
+    per_rank = [float(x.item()) for x in every]
+    return max(per_rank), per_rank
 
 
 def make_comm(ctx, rank, world):
@@ -265,10 +291,27 @@ def make_comm(ctx, rank, world):
     if world == 1:
         return None
     if dist.get_backend() != "nccl":
-        return ge.Comm(ctx, world, rank, backend="transport")
-    box = [ge.Comm.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
-    return ge.Comm(ctx, world, rank, backend="rccl", uid=box[0])
+        comm = ge.Comm(ctx, world, rank, backend="transport")
+    else:
+        box = [ge.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = ge.Comm(ctx, world, rank, backend="rccl", uid=box[0])
+    nranks, crank, is_rccl = comm.info()
+    assert nranks == world and crank == rank, (nranks, crank, world, rank)
+    assert bool(is_rccl) == (dist.get_backend() == "nccl"), "expected the RCCL communicator"
+    return comm
+
+
+def comm_record(comm, world):
+    """What the library's communicator reports (nranks_seen, RCCL or transport)."""
+    if comm is None:
+        return {"nranks_seen": 1, "backend": "none (one GPU)"}
+    nranks, _, is_rccl = comm.info()
+    rec = {"nranks_seen": nranks, "backend": "rccl" if is_rccl else "transport"}
+    if not is_rccl:
+        rec["rehearsal"] = ("ranks share one GPU over the host transport "
+                            "(GE_DIST_BACKEND=gloo): a rehearsal, not a multi-GPU measurement")
+    return rec
 
 
 def run_multilevel(args, rank, world, local, dev):
@@ -328,13 +371,16 @@ def run_multilevel(args, rank, world, local, dev):
         log(rank, f"aggregate shards: loads "
                   f"{[f'{cost[owner == r].sum():.3g}' for r in range(world)]}")
     plans = {}
+    plan_seconds = {}
 
     def plan_for(iters):
         if iters not in plans:
+            t0 = time.perf_counter()
             plans[iters] = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(),
                                        d["dx"].data_ptr(), PT[0], d["pip"].data_ptr(),
                                        d["pix"].data_ptr(), d["vA"].data_ptr(), args.dim,
                                        iterations=iters, aggs=mine if world > 1 else None)
+            plan_seconds[iters] = time.perf_counter() - t0
         return plans[iters]
 
     pk = plan_for(args.steps)
@@ -351,9 +397,15 @@ def run_multilevel(args, rank, world, local, dev):
         if comm is not None:  # one all-gather of the members' coordinates (libge, RCCL)
             comm.allgather_members(X.data_ptr(), args.dim, PT, owner)
 
-    elapsed = timed(args, world, dev, steps)
+    elapsed, per_rank = timed(args, world, dev, steps)
     rep_ms, rep_launches, rep_pairs = pk.repulse_ms()
     res_ms, str_ms, _ = pk.kernel_ms()
+    att_ms, att_passes, att_rows, att_entries = pk.rows_ms()
+    # SURVEY.md 8(d) B_attr over the streamed members' rows: indptr 4 B + x read 24 B +
+    # x write 24 B per row, 12 B per CSR entry (int32 index + fp64 weight)
+    att_bytes = 12 * att_entries + 52 * att_rows
+    att_gbs = att_bytes / (att_ms * 1e-3) / 1e9 if att_ms > 0 else 0.0
+    att_traffic, att_src = pmc_traffic_per_launch("FamlRows", args.workload)
     rep_kernel = "faml_big_repulse" if os.environ.get("GE_FAML_SYM") == "0" else "faml_sym_repulse"
     traffic, traffic_src = pmc_traffic_per_launch(rep_kernel, args.workload)
     finite = bool(torch.isfinite(X).all().item())
@@ -393,10 +445,27 @@ def run_multilevel(args, rank, world, local, dev):
                                        "symmetric kernel evaluates each unordered pair once "
                                        "and credits both ordered pairs",
                      "avg_launch_ms": rep_ms, "launches": rep_launches},
+        "roofline_attraction": {"kernel": "tile_rows_kernel<FamlRows> + heavy rows (the "
+                                          "streamed members' CSR attraction / external pull, "
+                                          "gravity, update; one pass per iteration)",
+                                "bound": "hbm", "achieved": att_gbs, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": att_gbs / HBM_PEAK_GBS,
+                                "traffic": att_traffic, "traffic_source": att_src,
+                                "algorithmic_bytes_per_launch": att_bytes,
+                                "bytes_per_unit": "12 per CSR entry + 52 per row (SURVEY.md 8(d))",
+                                "rows": att_rows, "entries": att_entries,
+                                "avg_launch_ms": att_ms, "launches": att_passes},
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
         "setup_seconds": {"graph_device": t_gen, "partition_device": t_part,
-                          "partition_host": t_part_host, "ptap_device": t_ptap},
+                          "partition_host": t_part_host, "ptap_device": t_ptap,
+                          "plan_build": plan_seconds.get(args.steps),
+                          "plan_build_note": "per-level tables built once per plan outside the "
+                                             "timed steps (pack tables, edge codes, internal "
+                                             "degrees of the streamed members)"},
+        "ranks": dict(comm_record(comm, world), per_rank_seconds=per_rank),
     }
+    if world > 1:
+        result["ranks"]["per_rank_load"] = [float(cost[owner == r].sum()) for r in range(world)]
     for p in plans.values():
         p.close()
     if comm is not None:
@@ -454,7 +523,7 @@ def run_single_level(args, rank, world, local, dev):
                 comm.allgather_coords(buf[1].data_ptr(), chunk, args.dim)
             buf.reverse()
 
-    elapsed = timed(args, world, dev, steps)
+    elapsed, per_rank = timed(args, world, dev, steps)
     rep_ms, att_ms, launches = plan.kernel_ms()
     finite = bool(torch.isfinite(buf[0][:n]).all().item())
     its = args.steps / elapsed
@@ -492,6 +561,8 @@ def run_single_level(args, rank, world, local, dev):
                                 "traffic": att_traffic, "traffic_source": att_src,
                                 "algorithmic_bytes_per_launch": attr_bytes,
                                 "avg_launch_ms": att_ms},
+        "ranks": dict(comm_record(comm, world), per_rank_seconds=per_rank,
+                      rows_per_rank=[b - a for a, b in shards]),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_fa(A, X0, args.cpu_baseline_seconds, rank)
@@ -504,17 +575,74 @@ def run_single_level(args, rank, world, local, dev):
         print(json.dumps(result), flush=True)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`--gpus N` without an outside launcher: run torch.distributed.run with N
+    ranks (one per GPU) as a CHILD process and return its exit code.  Nothing here
+    touches the GPU (counting devices does not initialise it on this image), and the
+    process is never replaced (no exec)."""
+    import subprocess
+    import torch
+    backend = os.environ.get("GE_DIST_BACKEND", "nccl")
+    if backend == "nccl" and not args.launch_check:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs one GPU per rank but {have} "
+                  "visible; GE_DIST_BACKEND=gloo rehearses the ranks on one GPU over the "
+                  "host transport (labelled a rehearsal in the JSON)", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, GE_BENCH_SPAWNED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(world, rank, local):
+    """--launch-check: every rank reports (rank, local rank, pid) over the process
+    group; rank 0 prints one JSON line.  No GPU work."""
+    import torch.distributed as dist
+    seen = [None] * world
+    if world > 1:
+        dist.all_gather_object(seen, (rank, local, os.getpid()))
+    else:
+        seen = [(rank, local, os.getpid())]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "nranks_seen": world,
+                          "backend": dist.get_backend() if world > 1 else "none",
+                          "spawned_by_bench": os.environ.get("GE_BENCH_SPAWNED") == "1",
+                          "ranks": [{"rank": r, "local_rank": lr, "pid": pid}
+                                    for r, lr, pid in seen]}), flush=True)
+
+
 def main():
     args = parse()
     args.n, args.draws = WORKLOADS[args.workload]
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: {world} ranks were launched for --gpus {args.gpus}")
     # GE_DIST_BACKEND=gloo rehearses N ranks on one GPU (ranks share cuda:0); the real
     # multi-GPU run is one rank per GPU over RCCL ("nccl")
     backend = os.environ.get("GE_DIST_BACKEND", "nccl")
+    if args.launch_check:
+        if world > 1:
+            dist.init_process_group("gloo")
+        launch_check(world, rank, local)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
     if world > 1:

@@ -426,6 +426,7 @@ int ge_force_atlas_dist(ge_comm* c, int n, const int* ip, const int* ix, const d
     GE_REQUIRE(dim >= 1 && dim <= 4, "dimension must be 1..4");
     GE_REQUIRE(iterations >= 0, "negative iteration count");
     GE_REQUIRE(n == 0 || (ip && ix && dx && ip[0] == 0), "bad CSR");
+    if (n > 0) ge::check_csr(n, ip, ix, dx);  // indices in range, as the one-GPU calls
     ge::DeviceGuard g(c->ctx);
     ge::fa_host_dist(c, n, ip, ix, dx, dim, coords, init_random != 0, iterations, *p);
   });
@@ -440,6 +441,7 @@ int ge_force_atlas_ml_dist(ge_comm* c, int n, const int* ip, const int* ix, cons
     GE_REQUIRE(p && pip && pix && vA && cA && rA && (coords || n == 0), "null argument");
     GE_REQUIRE(dim >= 1 && dim <= 4, "dimension must be 1..4");
     GE_REQUIRE(n == 0 || (ip && ix && dx && ip[0] == 0), "bad CSR");
+    if (n > 0) ge::check_csr(n, ip, ix, dx);  // indices in range, as the one-GPU calls
     GE_REQUIRE(m >= 0 && pip[0] == 0 && pip[m] == n, "P_T must have one entry per fine vertex");
     if (n == 0) return;
     ge::DeviceGuard g(c->ctx);
@@ -453,6 +455,7 @@ int ge_ptap_dist(ge_comm* c, int n, const int* ip, const int* ix, const double* 
     ge::check_comm(c);
     GE_REQUIRE(out && pip && pix, "null argument");
     GE_REQUIRE(n == 0 || (ip && ix && dx && ip[0] == 0), "bad CSR");
+    if (n > 0) ge::check_csr(n, ip, ix, dx);  // indices in range, as the one-GPU calls
     GE_REQUIRE(m >= 0 && pip[0] == 0 && pip[m] == n, "P_T must have one entry per fine vertex");
     ge::DeviceGuard g(c->ctx);
     hipStream_t s = c->ctx->stream;

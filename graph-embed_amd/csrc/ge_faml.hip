@@ -738,6 +738,9 @@ struct ge_faml_plan {
   size_t next_ev = 0;
   std::vector<hipEvent_t> rev;  // 2 per profiled repulsion launch
   size_t next_rev = 0;
+  std::vector<hipEvent_t> aev;  // 2 per profiled member-row pass (FamlRows)
+  size_t next_aev = 0;
+  long long streamed_entries = 0;  // CSR entries of the streamed members' rows
 };
 
 namespace ge {
@@ -813,6 +816,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     for (size_t q = 0; q < rows.size(); ++q) {
       const int v = h_ptix[rows[q]];
       deg[q] = h_ip[v + 1] - h_ip[v];
+      pl->streamed_entries += deg[q];
     }
     // the in-aggregate repulsion is not far above the external pulls (measured
     // at C3: every heavy row left the binade), so heavy rows store their terms
@@ -1067,9 +1071,22 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                                 pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
         }
         if (re) GE_HIP(hipEventRecord(re[1], ss));
+        hipEvent_t* ae = nullptr;
+        if (pl->profiling) {
+          if (pl->next_aev + 2 > pl->aev.size())
+            for (int k = 0; k < 256; ++k) {
+              hipEvent_t e;
+              GE_HIP(hipEventCreate(&e));
+              pl->aev.push_back(e);
+            }
+          ae = &pl->aev[pl->next_aev];
+          pl->next_aev += 2;
+          GE_HIP(hipEventRecord(ae[0], ss));
+        }
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
                              cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
         launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
+        if (ae) GE_HIP(hipEventRecord(ae[1], ss));
         std::swap(cur, nxt);
       }
       hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,
@@ -1111,6 +1128,7 @@ static void faml_plan_free(ge_faml_plan* pl) {
   if (pl->fork) (void)hipEventDestroy(pl->fork);
   for (hipEvent_t e : pl->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pl->rev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : pl->aev) (void)hipEventDestroy(e);
   delete pl;
 }
 
@@ -1238,6 +1256,7 @@ int ge_faml_plan_set_profiling(ge_faml_plan* pl, int enable) {
     pl->profiling = enable != 0;
     pl->next_ev = 0;
     pl->next_rev = 0;
+    pl->next_aev = 0;
   });
 }
 
@@ -1279,6 +1298,27 @@ int ge_faml_plan_repulse_ms(ge_faml_plan* pl, double* ms, int* launches, double*
     }
     *ms = cnt ? t / cnt : 0.0;
     *launches = cnt;
+  });
+}
+
+int ge_faml_plan_rows_ms(ge_faml_plan* pl, double* ms, int* passes, long long* rows,
+                         long long* entries) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && ms && passes && rows && entries, "null argument");
+    *rows = pl->nrows;
+    *entries = pl->streamed_entries;
+    ge::DeviceGuard g(pl->ctx);
+    GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+    double t = 0;
+    int cnt = 0;
+    for (size_t k = 0; k + 2 <= pl->next_aev; k += 2) {
+      float x = 0.f;
+      GE_HIP(hipEventElapsedTime(&x, pl->aev[k], pl->aev[k + 1]));
+      t += x;
+      ++cnt;
+    }
+    *ms = cnt ? t / cnt : 0.0;
+    *passes = cnt;
   });
 }
 

@@ -35,15 +35,26 @@ namespace ge {
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& msg) { g_last_error = msg; }
 
-namespace {
-
-constexpr double kEps = 0.00001;
-
+// Host CSR arguments: indptr starts at 0 and never decreases, every column index
+// is a row id (the kernels gather by it).  O(n + nnz), OpenMP.
 void check_csr(int n, const int* ip, const int* ix, const double* dx) {
   GE_REQUIRE(n >= 0, "negative row count");
   GE_REQUIRE(n == 0 || (ip && ix && dx), "null CSR array");
-  if (n > 0) GE_REQUIRE(ip[0] == 0 && ip[n] >= 0, "bad indptr");
+  if (n == 0) return;
+  GE_REQUIRE(ip[0] == 0 && ip[n] >= 0, "bad indptr");
+  long long bad_rows = 0, bad_cols = 0;
+#pragma omp parallel for reduction(+ : bad_rows) schedule(static)
+  for (int i = 0; i < n; ++i) bad_rows += ip[i + 1] < ip[i];
+  GE_REQUIRE(bad_rows == 0, "indptr decreases");
+  const long long nnz = ip[n];
+#pragma omp parallel for reduction(+ : bad_cols) schedule(static)
+  for (long long e = 0; e < nnz; ++e) bad_cols += (unsigned)ix[e] >= (unsigned)n;
+  GE_REQUIRE(bad_cols == 0, "column index out of range");
 }
+
+namespace {
+
+constexpr double kEps = 0.00001;
 
 inline double dist_to(const double* from, const double* to, int dim) {
   double acc = 0.0;
@@ -491,9 +502,18 @@ int ge_partition(ge_ctx* ctx, int n, const int* ip, const int* ix, const double*
     // with a context: the device path (integer weights, symmetric, ascending rows);
     // otherwise, or when the input needs it, the host path
     const char* force_host = std::getenv("GE_PARTITION_HOST");
-    if (ctx && !(force_host && *force_host && *force_host != '0'))
-      *out = ge::partition_device(ctx, n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
-                                  matching);
+    if (ctx && !(force_host && *force_host && *force_host != '0')) {
+      try {
+        *out = ge::partition_device(ctx, n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
+                                    matching);
+      } catch (const ge::Error& e) {
+        // device capacity / convergence limits (list pool, resolve rounds): the host
+        // path computes the same hierarchy
+        if (e.code != GE_ERR_STATE) throw;
+        std::fprintf(stderr, "ge_partition: %s; using the host path\n", e.what());
+        *out = nullptr;
+      }
+    }
     if (!*out)
       *out = ge::partition_incremental(n, ip, ix, dx, cf, printing != 0, positive != 0, stall,
                                        matching);

@@ -145,6 +145,8 @@ struct DeviceGuard {
 // libstdc++ uniform_real_distribution<double>(-1,1) over mt19937(seed); written
 // out explicitly (see ge_rng.cpp) and tested equal to std:: in tests.
 void uniform_stream(unsigned seed, size_t count, double* out);
+// Host CSR validation (indptr, index range); throws GE_ERR_ARG.
+void check_csr(int n, const int* ip, const int* ix, const double* dx);
 
 // Device entry points implemented in the .hip files, called by host drivers.
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,

@@ -46,6 +46,7 @@
 #include <iostream>
 #include <limits>
 #include <numeric>
+#include <memory>
 #include <vector>
 
 #include "ge_internal.hpp"
@@ -1092,7 +1093,8 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   }
 
   // ---- host mirrors of the order-dependent state (:1610-1620)
-  auto* h = new ge_hier();
+  std::unique_ptr<ge_hier> hier(new ge_hier());  // released on success only
+  ge_hier* h = hier.get();
   std::vector<int> used(n), pointer(n), id(n), basis(n);
   std::iota(used.begin(), used.end(), 0);
   pointer = id = basis = used;
@@ -1314,7 +1316,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     for (size_t l = 0; l < h->rows.size(); ++l)
       std::cout << "level " << l + 1 << ": " << h->rows[l] << " aggregates" << std::endl;
   }
-  return h;
+  return hier.release();
 }
 
 }  // namespace ge

@@ -296,7 +296,9 @@ bool radius_step_device(ge_ctx* ctx, int m, double* cA, double* rA, int dim, boo
     if (mc)
       hipLaunchKernelGGL(group_of_kernel, dim3(grid_for(mc)), dim3(256), 0, s, mc, dpip.p, dpix.p,
                          drAc.p, grp.p, r.p);
-    const long long cap = std::max(nnz / 2 + 1, 1);
+    // one event per stored entry at most (an asymmetric A_c, e.g. one triangle,
+    // emits up to nnz; a symmetric one nnz / 2)
+    const long long cap = std::max(nnz, 1);
     ei.alloc(cap);
     ej.alloc(cap);
     et.alloc(cap);

@@ -159,7 +159,14 @@ __device__ __forceinline__ void sym_handover(int t, int lane, int A, int ncols, 
 #pragma unroll
     for (int k = 0; k < D; ++k) agent_st(F + (cbase + qo) * D + k, o[k]);
   }
+  // Ordering (no acquire/release: an agent-scope release would write back the whole
+  // L2, ~every 64 steps): the sums are agent-scope stores (they bypass the per-XCD
+  // L2), s_waitcnt(0) waits until every one of them has completed at the memory
+  // side, and only then is the flag stored.  The signal fences keep the compiler
+  // from moving the stores across the wait or the flag store.
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0);  // every lane's sums are stored before the flag
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   if (lane == 0) __hip_atomic_store(tprog + t, A + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -276,9 +283,14 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const int ntiles = (ncols + 63) >> 6;
     bool ok_prev = true;
     for (int tt = 0; tt < ntiles; ++tt) {
-      if (A > 0)  // the sweeps 0..A-1 have written column tile A + tt back
+      if (A > 0) {  // the sweeps 0..A-1 have written column tile A + tt back
         while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
           __builtin_amdgcn_s_sleep(1);
+        // the F loads below are agent-scope (served past the L2) and issued only after
+        // the spin has seen the flag (the loop's exit depends on the loaded value); the
+        // fence keeps the compiler from hoisting them above the loop
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
       const int qc = 64 * tt + lane;
       const bool cv = qc < ncols;
       double xc[D], ic[D], dc = 0.0;  // a column past the aggregate is inert

@@ -108,6 +108,9 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.c_double), _ip]),
     "ge_faml_plan_repulse_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _ip,
                                                ctypes.POINTER(ctypes.c_double)]),
+    "ge_faml_plan_rows_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _ip,
+                                            ctypes.POINTER(ctypes.c_longlong),
+                                            ctypes.POINTER(ctypes.c_longlong)]),
     "ge_faml_plan_destroy": (ctypes.c_int, [_vp]),
     "ge_selftest_math": (ctypes.c_int, [_vp, ctypes.c_longlong, ctypes.c_ulonglong,
                                         ctypes.POINTER(ctypes.c_longlong)]),
@@ -542,6 +545,15 @@ class FamlPlan:
         _check(lib().ge_faml_plan_repulse_ms(self.h, ctypes.byref(a), ctypes.byref(c),
                                              ctypes.byref(p)))
         return a.value, c.value, p.value
+
+    def rows_ms(self):
+        """(average ms of one streamed member-row pass, passes profiled, rows, CSR
+        entries per pass)"""
+        a, c = ctypes.c_double(), ctypes.c_int()
+        r, e = ctypes.c_longlong(), ctypes.c_longlong()
+        _check(lib().ge_faml_plan_rows_ms(self.h, ctypes.byref(a), ctypes.byref(c),
+                                          ctypes.byref(r), ctypes.byref(e)))
+        return a.value, c.value, r.value, e.value
 
     def close(self):
         if self.h:

@@ -137,6 +137,11 @@ int ge_faml_plan_kernel_ms(ge_faml_plan* plan, double* resident_ms, double* stre
  * evaluates (sum of s(s-1) over the streamed aggregates); 0 launches if none. */
 int ge_faml_plan_repulse_ms(ge_faml_plan* plan, double* ms_per_launch, int* launches,
                             double* pairs_per_launch);
+/* Average device ms of one pass over the streamed members' rows (FamlRows: CSR
+ * attraction / external pull, :415-467, gravity and update, :469-530; one per
+ * iteration), the passes profiled, and the rows and CSR entries one pass reads. */
+int ge_faml_plan_rows_ms(ge_faml_plan* plan, double* ms_per_pass, int* passes,
+                         long long* rows, long long* entries);
 int ge_faml_plan_destroy(ge_faml_plan* plan);
 
 /* ---- coarsening hierarchy ----

@@ -16,6 +16,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -294,10 +296,13 @@ int orc_force_atlas_ml_aggs(int n, const int* I, const int* J, const double* D, 
   std::vector<double> draws(total);
   orc_uniform_stream(seed, total, draws.data());
   const int na = aggs ? n_aggs : m;
-
-#pragma omp parallel for schedule(dynamic, 1)
-  for (int x = 0; x < na; ++x) {
-    const int a = aggs ? aggs[x] : x;
+  // Aggregates are independent (the reference's `omp parallel for` over them,
+  // :340); inside one, the force rows of an iteration are independent too (each
+  // row's sum is its own serial loop), so an aggregate of kInnerRows members or
+  // more runs alone with its rows on the threads -- same arithmetic, and the C4/C5
+  // hub aggregates (4e4-1e5 members) no longer hold one thread for minutes.
+  constexpr int kInnerRows = 8192;
+  auto run_agg = [&](int a, bool inner) {
     const int base = PI[a];
     const int s = PI[a + 1] - PI[a];
     const int* v = PJ + base;
@@ -306,6 +311,7 @@ int orc_force_atlas_ml_aggs(int n, const int* I, const int* J, const double* D, 
         X[(size_t)v[i] * dim + k] = draws[(size_t)(base + i) * dim + k];
 
     std::vector<double> deg(s);  // :362-383, internal neighbours only
+#pragma omp parallel for schedule(dynamic, 64) if (inner)
     for (int i = 0; i < s; ++i) {
       double acc = 0.0;
       for (int e = I[v[i]]; e < I[v[i] + 1]; ++e)
@@ -316,6 +322,7 @@ int orc_force_atlas_ml_aggs(int n, const int* I, const int* J, const double* D, 
     std::vector<double> F((size_t)s * dim, 0.0), Fprev((size_t)s * dim, 0.0);
     const double* ca = cA + (size_t)a * dim;
     for (int it = 0; it < iterations; ++it) {
+#pragma omp parallel for schedule(dynamic, 64) if (inner)
       for (int i = 0; i < s; ++i) {
         double acc[kMaxDim];
         for (int k = 0; k < dim; ++k) acc[k] = 0.0;
@@ -386,6 +393,15 @@ int orc_force_atlas_ml_aggs(int n, const int* I, const int* J, const double* D, 
         double& x = X[(size_t)v[i] * dim + k];
         x = ca[k] + rA[a] * (x / biggest);
       }
+  };
+  for (int x = 0; x < na; ++x) {
+    const int a = aggs ? aggs[x] : x;
+    if (PI[a + 1] - PI[a] >= kInnerRows) run_agg(a, true);
+  }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int x = 0; x < na; ++x) {
+    const int a = aggs ? aggs[x] : x;
+    if (PI[a + 1] - PI[a] < kInnerRows) run_agg(a, false);
   }
   return 0;
 }
@@ -458,11 +474,15 @@ orc_hier* orc_partition(int n, const int* I, const int* J, const double* D, doub
     h->indices.push_back(std::move(ix));
   };
 
+  const bool progress = std::getenv("ORC_PROGRESS") != nullptr;  // long runs (C4 digest)
+  long rounds = 0;
   int M_prev = M;
   do {
     std::vector<std::pair<int, int>> merges;
     for (int pass = 0; pass < matching_iterations; ++pass) {
-      // scan (:1703-1726): argmax over untouched neighbours, ascending j, strict >
+      // scan (:1703-1726, `omp parallel for` there too): argmax over untouched
+      // neighbours, ascending j, strict >; each x writes only its own slots
+#pragma omp parallel for schedule(dynamic, 512)
       for (int x = 0; x < (int)used.size(); ++x) {
         const int i = used[x];
         if (touched[i] && best_eta[i] != -inf) continue;
@@ -526,6 +546,9 @@ orc_hier* orc_partition(int n, const int* I, const int* J, const double* D, doub
       touched[keep] = 0;
       M -= 1;
     }
+    if (progress && (++rounds % 50) == 0)
+      std::fprintf(stderr, "orc_partition: round %ld M %d levels %zu\n", rounds, M,
+                   h->rows.size());
   } while (1.0 * M / M_prev < stall);
   snapshot();
   return h;

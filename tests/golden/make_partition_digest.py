@@ -1,12 +1,20 @@
-"""Generates tests/golden/partition_c3_digest.json: the oracle's partition
-hierarchy of configs[2]'s graph (LCC of the R-MAT with 1M ids, 8M draws, seed
-12345), as level sizes + sha256 of the P_T arrays.  The oracle
-(oracle/ge_oracle.cpp, the reference loop of src/partitioner.cpp:1550-1893 restated
-with its std::map adjacency) takes ~21 minutes on 8 cores here, so only the digest
-is committed; tests/test_partition_device.py::test_partition_device_c3_digest
-checks the device hierarchy against it.
+"""Generates tests/golden/partition_<cfg>_digest.json: the oracle's partition
+hierarchy of a configs[] graph as level sizes + sha256 of the P_T arrays.
 
-usage: python tests/golden/make_partition_digest.py
+  c3  configs[2]: LCC of the R-MAT with 1M ids, 8M draws, seed 12345
+      (~21 minutes serial here, 2025; the scan is OpenMP-parallel like the
+      reference's :1703 since round 3)
+  c4  configs[3]: LCC of the R-MAT with 10M ids, 80M draws, seed 12345
+      (hours on 8 cores; run it in the background)
+
+The oracle (oracle/ge_oracle.cpp, the reference loop of src/partitioner.cpp:1550-1893
+restated with its std::map adjacency) is far too slow to run inside a test at
+these sizes, so only the digest is committed;
+tests/test_partition_device.py::test_partition_device_<cfg>_digest checks the
+device hierarchy against it.  The per-level sha256 values let a mismatch be
+localised to the first differing level.
+
+usage: python tests/golden/make_partition_digest.py [c3|c4]
 """
 import hashlib
 import json
@@ -24,22 +32,42 @@ import numpy as np  # noqa: E402
 import ge_amd as ge  # noqa: E402
 import oracle_lib as O  # noqa: E402
 
+CONFIGS = {"c3": (1_000_000, 8_000_000), "c4": (10_000_000, 80_000_000)}
+
+
+def digest(hier):
+    """(whole-hierarchy sha256, per-level sha256 list) of P_T indptr/indices."""
+    h = hashlib.sha256()
+    per = []
+    for lvl in hier:
+        ip = np.ascontiguousarray(lvl[0], dtype=np.int32).tobytes()
+        ix = np.ascontiguousarray(lvl[1], dtype=np.int32).tobytes()
+        h.update(ip)
+        h.update(ix)
+        per.append(hashlib.sha256(ip + ix).hexdigest())
+    return h.hexdigest(), per
+
 
 def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    n_ids, draws = CONFIGS[cfg]
+    seed, cf = 12345, 0.125
     O.build()
-    n_ids, draws, seed, cf = 1_000_000, 8_000_000, 12345, 0.125
     L = ge.largest_component(ge.rmat_csr(n_ids, draws, seed=seed))
+    print(f"{cfg}: LCC n={len(L[0]) - 1} nnz={len(L[1])}", flush=True)
     t = time.time()
     ho = O.partition(L, cf)
     el = time.time() - t
-    h = hashlib.sha256()
-    for ip, ix, _, _ in ho:
-        h.update(np.ascontiguousarray(ip, dtype=np.int32).tobytes())
-        h.update(np.ascontiguousarray(ix, dtype=np.int32).tobytes())
+    if os.environ.get("GE_DIGEST_SAVE"):  # keep the hierarchy itself (not committed)
+        np.savez(os.environ["GE_DIGEST_SAVE"],
+                 **{f"{k}{l}": a for l, h in enumerate(ho) for k, a in (("ip", h[0]), ("ix", h[1]))})
+    full, per = digest(ho)
     out = {"n_ids": n_ids, "draws": draws, "seed": seed, "cf": cf, "lcc_n": len(L[0]) - 1,
-           "lcc_nnz": len(L[1]), "rows": [x[2] for x in ho], "sha256": h.hexdigest(),
-           "oracle_seconds": round(el, 1), "generator": "tests/golden/make_partition_digest.py"}
-    with open(os.path.join(HERE, "partition_c3_digest.json"), "w") as f:
+           "lcc_nnz": len(L[1]), "rows": [x[2] for x in ho], "sha256": full,
+           "level_sha256": per, "oracle_seconds": round(el, 1),
+           "oracle_threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
+           "generator": f"tests/golden/make_partition_digest.py {cfg}"}
+    with open(os.path.join(HERE, f"partition_{cfg}_digest.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(out)
 

@@ -114,6 +114,65 @@ def test_c4_level0_sampled_aggregates(ctx, oracle):
     assert np.isfinite(got).all()
 
 
+def _coarse_rows_numpy(L, PT, vA, rows):
+    """Rows of P_T A P for the coarse ids `rows`, straight from the definition (entry
+    (a, b) = sum of a_ij over i in a, j in b): exact, since the
+    R-MAT weights are 1.0."""
+    ip, ix, dx = L
+    out = {}
+    for a in rows:
+        mem = PT[1][PT[0][a]:PT[0][a + 1]]
+        e = np.concatenate([np.arange(ip[i], ip[i + 1]) for i in mem])
+        b, w = np.unique(vA[ix[e]], return_inverse=True)
+        out[int(a)] = (b.astype(np.int32), np.bincount(w, weights=dx[e]))
+    return out
+
+
+def test_c5_level0_sampled_aggregates(ctx, oracle):
+    """configs[4] (C5) as an embed level: the 100M-id / 800M-draw R-MAT's LCC built
+    on the device (examples/embedder.cpp:35-93), partition(A, 0.125) on the device
+    (src/partitioner.cpp:1550-1893), P^T A P of level 0 on the device, and the
+    level-0 forceAtlasMultilevel call (include/forceatlas.hpp:314-574; 2 iterations,
+    symmetric streamed kernel at full size) against the oracle on the largest
+    aggregate, the streamed / resident boundary and random small aggregates.  The
+    coarse rows of the sampled aggregates are checked against their definition."""
+    import time
+    t0 = time.perf_counter()
+    L = ctx.rmat_csr(100_000_000, 800_000_000, seed=12345, lcc=True)
+    n, nnz = len(L[0]) - 1, len(L[1])
+    _progress(t0, f"C5 LCC n={n} nnz={nnz} (device)")
+    hier = ctx.partition(L, 0.125)
+    _progress(t0, f"C5 device partition levels {[h[2] for h in hier]}")
+    PT = hier[0]
+    m = PT[2]
+    assert PT[3] == n and len(PT[1]) == n
+    assert np.array_equal(np.sort(PT[1]), np.arange(n, dtype=np.int32))
+    vA = ge.vertex_of(PT)
+    C = ctx.ptap(L, PT)
+    _progress(t0, f"C5 device P^T A P nnz={len(C[1])}")
+    assert len(C[0]) == m + 1 and C[2].sum() == L[2].sum()
+    sizes = np.diff(PT[0])
+    order = np.argsort(sizes, kind="stable")
+    big = [int(order[-1])] + [int(a) for a in order if 2000 < sizes[a] <= 4000][:3]
+    split = [int(a) for a in order if 200 <= sizes[a] <= 2000][-4:]
+    small = np.random.default_rng(6).choice(np.nonzero(sizes <= 200)[0], 100, replace=False)
+    aggs = np.array(sorted(set(big) | set(split) | set(small.tolist())), dtype=np.int32)
+    for a, (b, w) in _coarse_rows_numpy(L, PT, vA, aggs).items():
+        assert np.array_equal(C[1][C[0][a]:C[0][a + 1]], b)
+        assert np.array_equal(C[2][C[0][a]:C[0][a + 1]], w)
+    del C
+    cA = ge.uniform_stream(7, m * 3).reshape(m, 3)
+    rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
+    got = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=2, seed=5)
+    _progress(t0, f"C5 device level done (largest aggregate {sizes.max()})")
+    want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
+    _progress(t0, "C5 oracle aggregates done")
+    rows = np.concatenate([PT[1][PT[0][a]:PT[0][a + 1]] for a in aggs])
+    assert sizes[aggs].max() == sizes.max()
+    assert np.array_equal(got[rows], want[rows])
+    assert np.isfinite(got).all()
+
+
 def test_c5_attraction_pass_sampled_rows(oracle):
     import time
     t0 = time.perf_counter()

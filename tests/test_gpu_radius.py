@@ -73,18 +73,22 @@ def _one_group(A, cA, oracle, ctx):
     return r1, c1, dev, r2, c2
 
 
-@pytest.mark.parametrize("shape", ["star", "path", "grid"])
+@pytest.mark.parametrize("shape", ["star", "path", "grid", "star_upper", "grid_upper"])
 def test_radius_group_shapes(ctx, oracle, shape):
+    """*_upper: A_c stores only its upper triangle (the reference accepts it,
+    src/embed.cpp:697-704): one event per stored entry, nnz events in all."""
     import scipy.sparse as sp
     m = 2000
+    upper = shape.endswith("_upper")
+    shape = shape.replace("_upper", "")
     if shape == "star":
         e = [(0, j) for j in range(1, m)]
     elif shape == "path":
         e = [(j, j + 1) for j in range(m - 1)]
     else:
         e = [(j, j + 1) for j in range(m - 1) if (j + 1) % 40] + [(j, j + 40) for j in range(m - 40)]
-    r = [a for a, b in e] + [b for a, b in e]
-    c = [b for a, b in e] + [a for a, b in e]
+    r = [a for a, b in e] + ([] if upper else [b for a, b in e])
+    c = [b for a, b in e] + ([] if upper else [a for a, b in e])
     M = sp.csr_matrix((np.ones(len(r)), (r, c)), shape=(m, m))
     M.sort_indices()
     A = (M.indptr.astype(np.int32), M.indices.astype(np.int32), M.data)
