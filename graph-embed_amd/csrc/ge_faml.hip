@@ -38,6 +38,7 @@
 #include "ge_pair.hpp"
 #include "ge_rows.hpp"
 #include "ge_sym.hpp"
+#include "ge_sym2.hpp"
 
 namespace ge {
 namespace {
@@ -479,6 +480,91 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
   }
 }
 
+// Row blocks of the largest streamed aggregates on CUs of their own.  A row block
+// spans its aggregate's whole width (every ordered pair of its 64 rows, partners
+// ascending: the plain scheme, no dependencies), so for an aggregate of T column
+// tiles it is a chain of T tile-times -- the launch's critical path once the
+// aggregate is large.  Launched with a dynamic LDS reservation that leaves no room
+// for another block on the CU, its 4 waves own their SIMDs; U partners per lane are
+// in flight at once (their terms added in j order) so a lone wave keeps issuing, and
+// the next column tile is loaded into registers while the current one is computed.
+// items = (aggregate, first row), 64 rows each; queue = one counter.
+template <int D, int U, bool REPEL_ONE>
+__global__ void __launch_bounds__(kHT)
+faml_lone_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ queue,
+                  const int* __restrict__ pt_ip, const double* __restrict__ Xp,
+                  const double* __restrict__ DP, double repel, double* __restrict__ Fscr) {
+  constexpr int WV = W<D>::v;
+  __shared__ __attribute__((aligned(16))) double tiles[kHT / 64][kBigW * WV];
+  const int lane = threadIdx.x & 63;
+  double* tile = tiles[threadIdx.x >> 6];
+  const bool repel_ok = REPEL_ONE || weight_ok(repel);
+  for (;;) {
+    int q = 0;
+    if (lane == 0) q = atomicAdd(queue, 1);
+    q = __builtin_amdgcn_readfirstlane(q);
+    if (q >= nitems) break;  // every wave leaves once the queue is drained
+    const int2 item = items[q];
+    const int base = pt_ip[item.x];
+    const int s = pt_ip[item.x + 1] - base;
+    const int li = item.y + lane;
+    const bool rv = li < s;
+    double xi[D], acc[D], di = 1.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xi[k] = rv ? Xp[((size_t)base + li) * D + k] : 0.0;
+      acc[k] = 0.0;
+    }
+    if (rv) di = DP[(size_t)base + li];
+    const bool rows_ok = repel_ok && __all(vertex_ok<D>(xi, di));
+    // partner record of this lane for the next tile, held in registers
+    double nx[D + 1];
+    auto fetch = [&](int j0) {
+      const bool v = j0 + lane < s;
+      const size_t c = (size_t)base + (v ? j0 + lane : 0);
+#pragma unroll
+      for (int k = 0; k < D; ++k) nx[k] = v ? Xp[c * D + k] : 0.0;
+      nx[D] = v ? DP[c] : 1.0;
+    };
+    fetch(0);
+    for (int j0 = 0; j0 < s; j0 += kBigW) {
+      const int cnt = min(kBigW, s - j0);
+      wave_lds_sync();  // the previous tile has been read by every lane
+#pragma unroll
+      for (int k = 0; k <= D; ++k) tile[lane * WV + k] = nx[k];
+      const bool ok = lane >= cnt || vertex_ok<D>(nx, nx[D]);
+      wave_lds_sync();
+      if (j0 + kBigW < s) fetch(j0 + kBigW);  // in flight while this tile computes
+      if (rows_ok && __all(ok)) {
+        int jj = 0;
+        if constexpr (U > 1) {
+          for (; jj + U <= cnt; jj += U) {
+            double t[U][D];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+              rep_term<D, true, REPEL_ONE>(xi, &tile[(jj + u) * WV], di, tile[(jj + u) * WV + D],
+                                           repel, t[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[u][k];
+          }
+        }
+        for (; jj < cnt; ++jj)  // the j == i term is +-0 (ge_pair.hpp)
+          rep_pair<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
+      } else {
+        for (int jj = 0; jj < cnt; ++jj)
+          rep_pair_fb<D, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel,
+                                    j0 + jj == li, acc);
+      }
+    }
+    if (rv) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) Fscr[((size_t)base + li) * D + k] = acc[k];
+    }
+  }
+}
+
 // Per streamed member, after faml_big_repulse: the CSR row (:415-467) added to
 // the repulsion sum in stored order (degree-classed, ge_rows.hpp), gravity
 // (:469-474) and the swing/speed update (:477-530).
@@ -722,8 +808,9 @@ struct ge_faml_plan {
   ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
-  // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters
-  bool sym = false;
+  // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters;
+  // sym2: each sweep spread over a workgroup (ge_sym2.hpp)
+  bool sym = false, sym2 = false;
   ge::DevBuf<int4> units;
   ge::DevBuf<int> prog;
   int nunits = 0, ntiles = 0, sym_blocks = 0;
@@ -741,6 +828,14 @@ struct ge_faml_plan {
   std::vector<hipEvent_t> aev;  // 2 per profiled member-row pass (FamlRows)
   size_t next_aev = 0;
   long long streamed_entries = 0;  // CSR entries of the streamed members' rows
+  // row blocks of the largest aggregates on CUs of their own (faml_lone_repulse),
+  // beside the sweeps, on their own stream
+  ge::DevBuf<int2> lone_items;
+  ge::DevBuf<int> lone_queue;
+  int nlone = 0, lone_blocks = 0, lone_U = 4;
+  size_t lone_lds = 0;
+  hipStream_t lone_st = nullptr;
+  hipEvent_t lone_fork = nullptr, lone_join = nullptr;
 };
 
 namespace ge {
@@ -845,6 +940,10 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     const char* e = std::getenv("GE_FAML_SYM");
     pl->sym = !(e && *e == '0');
   }
+  {
+    const char* e = std::getenv("GE_FAML_SYM2");
+    pl->sym2 = pl->sym && e && *e == '1';
+  }
   if (pl->sym && !big.empty()) {
     // The sweeps of an aggregate with T row tiles form a chain of ~2.5 T tile-times
     // (each sweep starts after its predecessor has passed its first two tiles); the
@@ -857,13 +956,18 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
+          &occ, pl->sym2 ? (const void*)faml_sym2_repulse<D, false>
+                         : (const void*)faml_sym_repulse<D, false>,
+          pl->sym2 ? kSym2T : kSymT, 0));
     });
     int bpc = std::min(std::max(occ, 1), 4);
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
-    const double waves = (double)pl->sym_blocks * (kSymT / 64);
+    // sweep slots: waves (ge_sym.hpp) or workgroups (ge_sym2.hpp, each sweep on a
+    // workgroup, advancing ~4x faster: tile-times below are the slot's own)
+    const double waves = pl->sym2 ? (double)pl->sym_blocks
+                                  : (double)pl->sym_blocks * (kSymT / 64);
     std::vector<size_t> by_T(big.size());
     std::iota(by_T.begin(), by_T.end(), 0);
     std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
@@ -879,7 +983,9 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // N = 4: 20 of 24 aggregates as row blocks 70 ms per iteration, 7 of 25 (4 090
     // row blocks) 58 ms, all 52 ms).
     // Take the count that minimises it.
-    double chain_k = 2.5, row_k = 0.8;
+    // sym2: a row block runs on one wave of a workgroup, ~4 workgroup tile-times per
+    // tile, so row blocks never shorten the critical path: all sweeps by default
+    double chain_k = pl->sym2 ? 0.0 : 2.5, row_k = 0.8;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
     double best = 1e300;
@@ -905,6 +1011,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         }
       }
       for (size_t k = 0; k < best_k; ++k) rows_mode[by_T[k]] = 1;
+      // GE_FAML_LONE=k: the k largest as lone row blocks instead (measurement knob)
+      if (const char* e = std::getenv("GE_FAML_LONE")) {
+        const size_t k = std::min(by_T.size(), (size_t)std::max(0, std::atoi(e)));
+        for (size_t q = 0; q < by_T.size(); ++q) rows_mode[by_T[q]] = q < k ? 2 : 0;
+      }
       if (std::getenv("GE_FAML_PLAN_DEBUG"))
         std::fprintf(stderr,
                      "faml plan: %zu streamed aggregates, T max %d, waves %.0f, work/waves %.1f "
@@ -927,8 +1038,41 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     }
     std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b)
-      if (rows_mode[b])
-        for (int A = 0; A < T[b]; ++A) rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
+      if (rows_mode[b] == 1)  // sym2: one unit = row tiles A .. A+3, one per wave
+        for (int A = 0; A < T[b]; A += pl->sym2 ? 4 : 1)
+          rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
+    std::vector<int2> lone;
+    for (size_t q = 0; q < by_T.size(); ++q)  // largest first
+      if (rows_mode[by_T[q]] == 2)
+        for (int A = 0; A < T[by_T[q]]; ++A) lone.push_back(make_int2(big[by_T[q]], 64 * A));
+    if (!lone.empty()) {
+      pl->nlone = (int)lone.size();
+      pl->lone_items.alloc(lone.size());
+      pl->lone_items.upload(lone.data(), lone.size(), st);
+      pl->lone_queue.alloc(std::max(pl->iterations, 1));
+      if (const char* e = std::getenv("GE_FAML_LONE_U")) pl->lone_U = std::atoi(e);
+      if (pl->lone_U != 1 && pl->lone_U != 2 && pl->lone_U != 4) pl->lone_U = 4;
+      // one block of 4 waves per CU and no other block beside it: reserve LDS past
+      // what a second block of any streamed kernel could find (160 KiB per CU)
+      pl->lone_lds = 120 * 1024;
+      if (const char* e = std::getenv("GE_FAML_LONE_LDS")) pl->lone_lds = std::atoi(e);
+      pl->lone_blocks = std::min(cus, (pl->nlone + 3) / 4);
+      dispatch_dim(dim, [&](auto Dc) {
+        constexpr int D = decltype(Dc)::value;
+        const void* ks[] = {(const void*)faml_lone_repulse<D, 1, true>,
+                            (const void*)faml_lone_repulse<D, 2, true>,
+                            (const void*)faml_lone_repulse<D, 4, true>,
+                            (const void*)faml_lone_repulse<D, 1, false>,
+                            (const void*)faml_lone_repulse<D, 2, false>,
+                            (const void*)faml_lone_repulse<D, 4, false>};
+        for (const void* k : ks)
+          GE_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)pl->lone_lds));
+      });
+      GE_HIP(hipStreamCreateWithFlags(&pl->lone_st, hipStreamNonBlocking));
+      GE_HIP(hipEventCreateWithFlags(&pl->lone_fork, hipEventDisableTiming));
+      GE_HIP(hipEventCreateWithFlags(&pl->lone_join, hipEventDisableTiming));
+    }
     // row blocks have no dependencies and each spans its aggregate's whole width:
     // first in the queue (measured on per-rank shares of C4: N = 4 69 ms per
     // iteration against 80 ms when spread among the sweeps, N = 2 unchanged)
@@ -1012,6 +1156,25 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   GE_HIP(hipStreamSynchronize(st));
 }
 
+template <int D>
+static void launch_lone(ge_faml_plan* pl, int it, const double* X, double repel) {
+  const dim3 g(pl->lone_blocks), b(kHT);
+  int* q = pl->lone_queue.p + it;
+#define GE_LONE(UU)                                                                              \
+  if (repel == 1.0)                                                                              \
+    hipLaunchKernelGGL((faml_lone_repulse<D, UU, true>), g, b, pl->lone_lds, pl->lone_st,        \
+                       pl->nlone, pl->lone_items.p, q, pl->pt_ip, X, pl->DP.p, repel, pl->Fscr.p); \
+  else                                                                                           \
+    hipLaunchKernelGGL((faml_lone_repulse<D, UU, false>), g, b, pl->lone_lds, pl->lone_st,       \
+                       pl->nlone, pl->lone_items.p, q, pl->pt_ip, X, pl->DP.p, repel, pl->Fscr.p);
+  switch (pl->lone_U) {
+    case 1: GE_LONE(1) break;
+    case 2: GE_LONE(2) break;
+    default: GE_LONE(4) break;
+  }
+#undef GE_LONE
+}
+
 static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, const double* init,
                           double* X) {
   hipStream_t st = pl->ctx->stream;
@@ -1041,6 +1204,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
                          nr, pl->rows.p, init, pl->Xa.p, pl->Fprev.p);
       GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
+      if (pl->nlone > 0) GE_HIP(hipMemsetAsync(pl->lone_queue.p, 0, sizeof(int) * iters, ss));
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
@@ -1056,7 +1220,23 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_rev += 2;
           GE_HIP(hipEventRecord(re[0], ss));
         }
-        if (pl->sym) {
+        if (pl->nlone > 0) {  // lone row blocks first: their CUs are taken before the sweeps'
+          GE_HIP(hipEventRecord(pl->lone_fork, ss));
+          GE_HIP(hipStreamWaitEvent(pl->lone_st, pl->lone_fork, 0));
+          launch_lone<D>(pl, it, cur, c.repel);
+          GE_HIP(hipEventRecord(pl->lone_join, pl->lone_st));
+        }
+        if (pl->sym2) {
+          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
+          if (c.repel == 1.0)
+            hipLaunchKernelGGL((faml_sym2_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSym2T),
+                               0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+          else
+            hipLaunchKernelGGL((faml_sym2_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSym2T),
+                               0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+        } else if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
           if (c.repel == 1.0)
             hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
@@ -1070,6 +1250,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                                 pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
         }
+        if (pl->nlone > 0) GE_HIP(hipStreamWaitEvent(ss, pl->lone_join, 0));
         if (re) GE_HIP(hipEventRecord(re[1], ss));
         hipEvent_t* ae = nullptr;
         if (pl->profiling) {
@@ -1126,6 +1307,12 @@ static void faml_plan_free(ge_faml_plan* pl) {
     if (pl->join[k]) (void)hipEventDestroy(pl->join[k]);
   }
   if (pl->fork) (void)hipEventDestroy(pl->fork);
+  if (pl->lone_st) {
+    (void)hipStreamSynchronize(pl->lone_st);
+    (void)hipStreamDestroy(pl->lone_st);
+  }
+  if (pl->lone_fork) (void)hipEventDestroy(pl->lone_fork);
+  if (pl->lone_join) (void)hipEventDestroy(pl->lone_join);
   for (hipEvent_t e : pl->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pl->rev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pl->aev) (void)hipEventDestroy(e);

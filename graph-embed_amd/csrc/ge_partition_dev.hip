@@ -880,7 +880,7 @@ __global__ void init_lists_kernel(int n, const int* __restrict__ ip, const int* 
         int lo = ip[j], hi = ip[j + 1] - 1;
         bool found = false;
         while (lo <= hi) {
-          const int mid = (lo + hi) >> 1;
+          const int mid = lo + ((hi - lo) >> 1);  // entry offsets reach 2^31 / 2 (C5)
           const int c = ix[mid];
           if (c == i) {
             found = dx[mid] == w;
@@ -978,11 +978,16 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DeviceGuard guard(ctx);
   hipStream_t st = ctx->stream;
   const bool prof = std::getenv("GE_PROFILE_PARTITION") != nullptr;
+  // GE_PROGRESS: a line on stderr every ~10 s (long device runs, e.g. C5, stay visibly alive)
+  const bool progress = std::getenv("GE_PROGRESS") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto secs = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
     return std::chrono::duration<double>(b - a).count();
   };
   const auto t_start = now();
+  auto note = [&](const char* what) {
+    if (progress) std::fprintf(stderr, "partition_device: %s (%.1f s)\n", what, secs(t_start, now()));
+  };
   const long long nnz = I[n];
   // ---- buffers
   DevBuf<int> d_ip(n + 1), d_ix(std::max<long long>(nnz, 1));
@@ -990,6 +995,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d_ip.upload(I, n + 1, st);
   d_ix.upload(J, nnz, st);
   d_dx.upload(Dv, nnz, st);
+  note("input uploaded");
   const long long pool_cap = 3 * nnz + 4 * (long long)n + 1024;
   DevBuf<int> key_a(pool_cap), key_b(pool_cap);
   DevBuf<double> w_a(pool_cap), w_b(pool_cap);
@@ -1052,6 +1058,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d.pool_top = tops.p;
   d.pool_cap = pool_cap;
 
+  note("buffers allocated");
   GE_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * NCNT, st));
   GE_HIP(hipMemsetAsync(sums.p, 0, sizeof(double) * 2, st));
   GE_HIP(hipMemsetAsync(lk.p, 0x7F, sizeof(int) * n, st));
@@ -1063,6 +1070,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   GE_HIP(hipMemcpyAsync(&bad, cnt.p + C_BAD, sizeof(int), hipMemcpyDeviceToHost, st));
   GE_HIP(hipMemcpyAsync(h_sums, sums.p, sizeof(h_sums), hipMemcpyDeviceToHost, st));
   GE_HIP(hipStreamSynchronize(st));
+  note("lists built");
   if (bad || !(h_sums[0] < 4503599627370496.0)) return nullptr;  // sum |w| < 2^52
   {
     bool pos = true;
@@ -1160,6 +1168,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   int rounds = 0, compactions = 0;
   std::vector<MergeRec> order;
   std::vector<int> stamp(n, 0), moved(n / 2 + 1);
+  auto t_last_note = now();
   long long stat[NCNT] = {0};
   do {
     ++rounds;
@@ -1293,6 +1302,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       alist_len = M;
     }
     t_host += secs(t1, now());
+    if (progress && (rounds <= 3 || secs(t_last_note, now()) > 10.0)) {
+      t_last_note = now();
+      std::fprintf(stderr, "partition_device: round %d, %d aggregates, %lld merges, %.0f s\n",
+                   rounds, M, total_merges, secs(t_start, t_last_note));
+    }
     if (prof && std::getenv("GE_PROFILE_ROUNDS"))
       std::fprintf(stderr, "round %d alive %d merges %d pool %llu\n", rounds, M, nm, rb.top);
   } while (1.0 * M / M_prev < stall);  // :1838

@@ -115,11 +115,13 @@ __device__ __forceinline__ void sym_fetch(int sg, int lane, const double* rec, c
   constexpr int WV = SymW<D>::v;
   constexpr int IW = SymI<D>::v;
   const double* ic = ini + (sg & (kSymRing - 1)) * IW;
-  const double* xs = rec + ((sg - lane) & (kSymRing - 1)) * WV;
+  // records are stored by component (rec[k][slot]): consecutive lanes read
+  // consecutive slots, no bank conflicts
+  const int slot = (sg - lane) & (kSymRing - 1);
 #pragma unroll
   for (int k = 0; k < D; ++k) i0[k] = ic[k];
 #pragma unroll
-  for (int k = 0; k <= D; ++k) xv[k] = xs[k];
+  for (int k = 0; k <= D; ++k) xv[k] = rec[k * kSymRing + slot];
 }
 
 // Steps [s0, s1) of a sweep.  DIAG: the steps may meet the diagonal tile
@@ -301,14 +303,14 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       }
       if (cv) dc = DP[cbase + qc];
       const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
-      double* rs = rec + (qc & (kSymRing - 1)) * WV;
+      double* rs = rec + (qc & (kSymRing - 1));
       double* is = ini + (qc & (kSymRing - 1)) * IW;
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        rs[k] = xc[k];
+        rs[k * kSymRing] = xc[k];
         is[k] = ic[k];
       }
-      rs[D] = dc;
+      rs[D * kSymRing] = dc;
       wave_lds_sync();
       // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
       const bool fast = rows_ok && ok_cur && ok_prev;
@@ -323,10 +325,10 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
     }
     {  // drain: the last columns cross the wave; the slots past them hold inert records
-      double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1)) * WV;
+      double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1));
       double* is = ini + ((64 * ntiles + lane) & (kSymRing - 1)) * IW;
 #pragma unroll
-      for (int k = 0; k <= D; ++k) rs[k] = 0.0;
+      for (int k = 0; k <= D; ++k) rs[k * kSymRing] = 0.0;
 #pragma unroll
       for (int k = 0; k < D; ++k) is[k] = 0.0;
       wave_lds_sync();

@@ -30,6 +30,10 @@ def main():
              cA=T(ge.uniform_stream(7, m * dim)), rA=T(0.01 + 0.19 * (ge.uniform_stream(8, m) + 1) / 2),
              init=T(ge.uniform_stream(5, n0 * dim)))
     X = torch.zeros((n0, dim), dtype=torch.float64, device=dev)
+    if os.environ.get("SAVE_LEVEL"):  # level-0 sizes + members' CSR entries, for offline models
+        deg = np.diff(L[0]).astype(np.int64)
+        ent = np.add.reduceat(deg[PT[1]], PT[0][:-1])
+        np.savez(os.environ["SAVE_LEVEL"], pt_ip=PT[0], entries=ent)
     t1 = None
     for N in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
         owner = ge.assign_aggregates(PT, L[0], N)

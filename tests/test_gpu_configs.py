@@ -136,12 +136,17 @@ def test_c5_level0_sampled_aggregates(ctx, oracle):
     symmetric streamed kernel at full size) against the oracle on the largest
     aggregate, the streamed / resident boundary and random small aggregates.  The
     coarse rows of the sampled aggregates are checked against their definition."""
+    import os
     import time
+    os.environ["GE_PROGRESS"] = "1"  # the device partition reports every ~10 s
     t0 = time.perf_counter()
     L = ctx.rmat_csr(100_000_000, 800_000_000, seed=12345, lcc=True)
     n, nnz = len(L[0]) - 1, len(L[1])
     _progress(t0, f"C5 LCC n={n} nnz={nnz} (device)")
-    hier = ctx.partition(L, 0.125)
+    try:
+        hier = ctx.partition(L, 0.125)
+    finally:
+        del os.environ["GE_PROGRESS"]
     _progress(t0, f"C5 device partition levels {[h[2] for h in hier]}")
     PT = hier[0]
     m = PT[2]
