@@ -249,11 +249,14 @@ int orc_force_atlas(int n, const int* I, const int* J, const double* D, int dim,
   degrees(n, I, D, p.use_weights != 0, deg.data());
   std::vector<double> F((size_t)n * dim, 0.0), Fprev((size_t)n * dim, 0.0);
 
+  // rows are independent within an iteration; small levels (the coarsest, 1e5
+  // iterations) stay on one thread: a fork/join per iteration would dominate
+  const bool par = n >= 256;
   for (int it = 0; it < iterations; ++it) {
-#pragma omp parallel for schedule(dynamic, 16)
+#pragma omp parallel for schedule(dynamic, 16) if (par)
     for (int i = 0; i < n; ++i)
       fa_force_row(i, n, I, J, D, dim, X, deg.data(), p, &F[(size_t)i * dim]);
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) if (par)
     for (int i = 0; i < n; ++i)
       fa_update_vertex(X + (size_t)i * dim, &F[(size_t)i * dim], &Fprev[(size_t)i * dim],
                        dim, p, false);
