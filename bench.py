@@ -361,10 +361,13 @@ def run_multilevel(args, rank, world, local, dev):
     ctx.set_stream(work.cuda_stream)
     torch.cuda.synchronize(dev)
     comm = make_comm(ctx, rank, world)
-    # aggregates dealt to ranks by cost inside libge (ge_assign_aggregates: LPT on
-    # s(s-1) + the members' CSR entries)
-    owner = ge.assign_aggregates(PT, L[0], world)
+    # aggregates dealt to ranks by cost inside libge (ge_assign_aggregates_split: LPT
+    # on s(s-1) + the members' CSR entries; an aggregate above half a rank's share is
+    # split by row tiles over all ranks, owner -1, its rows exchanged every iteration)
+    owner = ge.assign_aggregates_split(PT, L[0], world) if world > 1 else np.zeros(m, np.int32)
     mine = np.flatnonzero(owner == rank).astype(np.int32)
+    split = np.flatnonzero(owner < 0).astype(np.int32)
+    gather_owner = np.where(owner < 0, 0, owner).astype(np.int32)
     if world > 1:
         from ge_amd.dist import aggregate_cost
         cost = aggregate_cost(PT[0], L[0], PT[1])
@@ -379,7 +382,8 @@ def run_multilevel(args, rank, world, local, dev):
             plans[iters] = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(),
                                        d["dx"].data_ptr(), PT[0], d["pip"].data_ptr(),
                                        d["pix"].data_ptr(), d["vA"].data_ptr(), args.dim,
-                                       iterations=iters, aggs=mine if world > 1 else None)
+                                       iterations=iters, aggs=mine if world > 1 else None,
+                                       split=split if world > 1 else None, comm=comm)
             plan_seconds[iters] = time.perf_counter() - t0
         return plans[iters]
 
@@ -395,7 +399,7 @@ def run_multilevel(args, rank, world, local, dev):
             p.set_profiling(True)
         p.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
         if comm is not None:  # one all-gather of the members' coordinates (libge, RCCL)
-            comm.allgather_members(X.data_ptr(), args.dim, PT, owner)
+            comm.allgather_members(X.data_ptr(), args.dim, PT, gather_owner)
 
     elapsed, per_rank = timed(args, world, dev, steps)
     rep_ms, rep_launches, rep_pairs = pk.repulse_ms()
@@ -465,7 +469,9 @@ def run_multilevel(args, rank, world, local, dev):
         "ranks": dict(comm_record(comm, world), per_rank_seconds=per_rank),
     }
     if world > 1:
-        result["ranks"]["per_rank_load"] = [float(cost[owner == r].sum()) for r in range(world)]
+        result["ranks"]["per_rank_load"] = [float(cost[owner == r].sum() + cost[owner < 0].sum() /
+                                                  world) for r in range(world)]
+        result["ranks"]["split_aggregates"] = int(len(split))
     for p in plans.values():
         p.close()
     if comm is not None:

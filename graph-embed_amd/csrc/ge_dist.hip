@@ -47,11 +47,12 @@ void abi(int rc) {
 
 ncclComm_t nccl_of(const ge_comm* c) { return (ncclComm_t)c->nccl; }
 
+}  // namespace
+
 // All-gather of equal blocks of `bytes` bytes between device buffers (d_send may
-// be d_recv + rank * bytes: in place).  Enqueued on the context's stream; the
-// transport path synchronises.
-void allgather_dev(ge_comm* c, const void* d_send, void* d_recv, size_t bytes) {
-  hipStream_t s = c->ctx->stream;
+// be d_recv + rank * bytes: in place), enqueued on stream s; the transport path
+// synchronises s.
+void allgather_stream(ge_comm* c, hipStream_t s, const void* d_send, void* d_recv, size_t bytes) {
   char* recv = (char*)d_recv;
   if (c->nranks == 1) {
     if (d_send != d_recv && bytes)
@@ -69,6 +70,13 @@ void allgather_dev(ge_comm* c, const void* d_send, void* d_recv, size_t bytes) {
     throw Error(GE_ERR_STATE, "transport all-gather failed");
   if (bytes) GE_HIP(hipMemcpyAsync(recv, hr.data(), bytes * c->nranks, hipMemcpyHostToDevice, s));
   GE_HIP(hipStreamSynchronize(s));
+}
+
+namespace {
+
+// The same on the context's stream.
+void allgather_dev(ge_comm* c, const void* d_send, void* d_recv, size_t bytes) {
+  allgather_stream(c, c->ctx->stream, d_send, d_recv, bytes);
 }
 
 // All-gather of small host arrays (counts, sizes).
@@ -148,9 +156,8 @@ void check_comm(const ge_comm* c) {
 
 }  // namespace
 
-// Longest-processing-time list scheduling of aggregates.
-std::vector<int> assign_aggregates(int m, const int* pip, const int* pix, const int* ip,
-                                   int nranks) {
+// Cost of an aggregate per iteration: ordered pairs + its members' CSR entries.
+std::vector<double> aggregate_costs(int m, const int* pip, const int* pix, const int* ip) {
   std::vector<double> cost(m);
   for (int a = 0; a < m; ++a) {
     const double s = pip[a + 1] - pip[a];
@@ -162,14 +169,23 @@ std::vector<int> assign_aggregates(int m, const int* pip, const int* pix, const 
     }
     cost[a] = c;
   }
-  std::vector<int> order(m);
-  for (int a = 0; a < m; ++a) order[a] = a;
+  return cost;
+}
+
+// Longest-processing-time list scheduling of aggregates; split
+// aggregates (split[a] != 0) get owner -1 and load every rank with an equal share.
+std::vector<int> assign_aggregates(int m, const int* pip, const int* pix, const int* ip,
+                                   int nranks, const std::vector<char>* split) {
+  const std::vector<double> cost = aggregate_costs(m, pip, pix, ip);
+  std::vector<int> order;
+  for (int a = 0; a < m; ++a)
+    if (!split || !(*split)[a]) order.push_back(a);
   std::stable_sort(order.begin(), order.end(),
                    [&](int x, int y) { return cost[x] > cost[y]; });  // ties: lower id first
   using Load = std::pair<double, int>;  // (load, rank): least load, then lowest rank
   std::priority_queue<Load, std::vector<Load>, std::greater<Load>> heap;
   for (int r = 0; r < nranks; ++r) heap.emplace(0.0, r);
-  std::vector<int> owner(m, 0);
+  std::vector<int> owner(m, -1);
   for (int a : order) {
     const Load top = heap.top();
     heap.pop();
@@ -207,6 +223,48 @@ void allgather_members(ge_comm* c, double* d_x, int dim, int m, const int* pip, 
                      dim, d_counts.p, d_first.p, d_rows.p, recv.p, d_x);
   GE_HIP(hipGetLastError());
   GE_HIP(hipStreamSynchronize(s));
+}
+
+// Rows of d_x listed per rank (d_rows: rank r's h_counts[r] positions from
+// h_first[r]) exchanged so every rank holds every rank's rows: pack this rank's into
+// its block of d_buf (nranks x width x dim), all-gather on stream s, unpack the
+// others.  Stream-ordered (RCCL); the transport path synchronises s.
+void exchange_rows(ge_comm* c, hipStream_t s, int dim, const int* d_rows, const int* d_counts,
+                   const int* d_first, const int* h_counts, const int* h_first, int width,
+                   double* d_buf, double* d_x) {
+  const int N = c->nranks;
+  double* mine = d_buf + (size_t)width * dim * c->rank;
+  const long long own = (long long)h_counts[c->rank] * dim;
+  if (own)
+    hipLaunchKernelGGL(pack_rows_kernel, dim3(grid_for(own)), dim3(256), 0, s, h_counts[c->rank],
+                       dim, d_rows + h_first[c->rank], d_x, mine);
+  allgather_stream(c, s, mine, d_buf, sizeof(double) * (size_t)width * dim);
+  const long long all = (long long)width * dim * N;
+  hipLaunchKernelGGL(unpack_rows_kernel, dim3(grid_for(all)), dim3(256), 0, s, N, c->rank, width,
+                     dim, d_counts, d_first, d_rows, d_buf, d_x);
+  GE_HIP(hipGetLastError());
+}
+
+// Aggregates split by row tiles across ranks: an aggregate whose
+// ordered pairs s(s-1) exceed half of a rank's average load cannot be balanced as a
+// whole.  min_members > 0 splits every aggregate of at least that many members
+// (tests); 0 splits none; < 0 the automatic rule (GE_DIST_SPLIT_MIN overrides it).
+std::vector<char> split_aggregates(int m, const int* pip, const int* pix, const int* ip,
+                                   int nranks, int min_members) {
+  std::vector<char> out(m, 0);
+  if (nranks <= 1) return out;
+  if (min_members < 0)
+    if (const char* e = std::getenv("GE_DIST_SPLIT_MIN")) min_members = std::atoi(e);
+  if (min_members > 0) {
+    for (int a = 0; a < m; ++a) out[a] = pip[a + 1] - pip[a] >= std::max(min_members, 2);
+    return out;
+  }
+  if (min_members == 0) return out;
+  const std::vector<double> cost = aggregate_costs(m, pip, pix, ip);
+  double W = 0.0;
+  for (double c : cost) W += c;
+  for (int a = 0; a < m; ++a) out[a] = pip[a + 1] - pip[a] >= 128 && cost[a] > 0.5 * W / nranks;
+  return out;
 }
 
 void fa_host_dist(ge_comm* c, int n, const int* ip, const int* ix, const double* dx, int dim,
@@ -254,10 +312,16 @@ void faml_host_dist(ge_comm* c, int n, const int* ip, const int* ix, const doubl
     faml_host(c->ctx, n, ip, ix, dx, m, pip, pix, vA, cA, rA, X, dim, iterations, p);
     return;
   }
-  const std::vector<int> owner = assign_aggregates(m, pip, pix, ip, c->nranks);
-  std::vector<int> mine;
-  for (int a = 0; a < m; ++a)
-    if (owner[a] == c->rank) mine.push_back(a);
+  // aggregates too large for a rank's share are split by row tiles over all ranks
+  // (their members exchanged after every iteration inside the plan); the rest are
+  // dealt whole by cost
+  const std::vector<char> split = split_aggregates(m, pip, pix, ip, c->nranks, -1);
+  std::vector<int> owner = assign_aggregates(m, pip, pix, ip, c->nranks, &split);
+  std::vector<int> mine, shared;
+  for (int a = 0; a < m; ++a) {
+    if (split[a]) shared.push_back(a);
+    else if (owner[a] == c->rank) mine.push_back(a);
+  }
   hipStream_t s = c->ctx->stream;
   std::vector<double> init((size_t)pip[m] * dim);
   uniform_stream(p.seed, init.size(), init.data());  // P_T storage order (:356-360)
@@ -272,15 +336,16 @@ void faml_host_dist(ge_comm* c, int n, const int* ip, const int* ix, const doubl
   drA.upload(rA, m, s);
   dinit.upload(init.data(), init.size(), s);
   GE_HIP(hipMemsetAsync(dX.p, 0, sizeof(double) * dX.n, s));
-  if (!mine.empty()) {
+  if (!mine.empty() || !shared.empty()) {
     ge_faml_plan* plan = nullptr;
-    abi(ge_faml_plan_create_subset(c->ctx, n, A.ip.p, A.ix.p, A.dx.p, m, pip, dpip.p, dpix.p,
-                                   dvA.p, dim, &p, iterations, mine.data(), (int)mine.size(),
-                                   &plan));
+    abi(ge_faml_plan_create_shard(c->ctx, c, n, A.ip.p, A.ix.p, A.dx.p, m, pip, dpip.p, dpix.p,
+                                  dvA.p, dim, &p, iterations, mine.data(), (int)mine.size(),
+                                  shared.data(), (int)shared.size(), &plan));
     const int rc = ge_faml_plan_run(plan, dcA.p, drA.p, dinit.p, dX.p);
     ge_faml_plan_destroy(plan);
     abi(rc);
   }
+  for (int a : shared) owner[a] = 0;  // every rank holds the split aggregates' members
   allgather_members(c, dX.p, dim, m, pip, pix, owner.data());
   dX.download(X, (size_t)n * dim, s);
   GE_HIP(hipStreamSynchronize(s));
@@ -401,7 +466,17 @@ int ge_assign_aggregates(int m, const int* pip, const int* pix, const int* ip, i
                          int* owner) {
   return guarded([&] {
     GE_REQUIRE(m >= 0 && pip && (pix || !ip) && owner && nranks >= 1, "bad arguments");
-    const std::vector<int> o = ge::assign_aggregates(m, pip, pix, ip, nranks);
+    const std::vector<int> o = ge::assign_aggregates(m, pip, pix, ip, nranks, nullptr);
+    std::copy(o.begin(), o.end(), owner);
+  });
+}
+
+int ge_assign_aggregates_split(int m, const int* pip, const int* pix, const int* ip, int nranks,
+                               int min_members, int* owner) {
+  return guarded([&] {
+    GE_REQUIRE(m >= 0 && pip && (pix || !ip) && owner && nranks >= 1, "bad arguments");
+    const std::vector<char> split = ge::split_aggregates(m, pip, pix, ip, nranks, min_members);
+    const std::vector<int> o = ge::assign_aggregates(m, pip, pix, ip, nranks, &split);
     std::copy(o.begin(), o.end(), owner);
   });
 }

@@ -38,7 +38,6 @@
 #include "ge_pair.hpp"
 #include "ge_rows.hpp"
 #include "ge_sym.hpp"
-#include "ge_sym2.hpp"
 
 namespace ge {
 namespace {
@@ -480,91 +479,6 @@ faml_big_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ q
   }
 }
 
-// Row blocks of the largest streamed aggregates on CUs of their own.  A row block
-// spans its aggregate's whole width (every ordered pair of its 64 rows, partners
-// ascending: the plain scheme, no dependencies), so for an aggregate of T column
-// tiles it is a chain of T tile-times -- the launch's critical path once the
-// aggregate is large.  Launched with a dynamic LDS reservation that leaves no room
-// for another block on the CU, its 4 waves own their SIMDs; U partners per lane are
-// in flight at once (their terms added in j order) so a lone wave keeps issuing, and
-// the next column tile is loaded into registers while the current one is computed.
-// items = (aggregate, first row), 64 rows each; queue = one counter.
-template <int D, int U, bool REPEL_ONE>
-__global__ void __launch_bounds__(kHT)
-faml_lone_repulse(int nitems, const int2* __restrict__ items, int* __restrict__ queue,
-                  const int* __restrict__ pt_ip, const double* __restrict__ Xp,
-                  const double* __restrict__ DP, double repel, double* __restrict__ Fscr) {
-  constexpr int WV = W<D>::v;
-  __shared__ __attribute__((aligned(16))) double tiles[kHT / 64][kBigW * WV];
-  const int lane = threadIdx.x & 63;
-  double* tile = tiles[threadIdx.x >> 6];
-  const bool repel_ok = REPEL_ONE || weight_ok(repel);
-  for (;;) {
-    int q = 0;
-    if (lane == 0) q = atomicAdd(queue, 1);
-    q = __builtin_amdgcn_readfirstlane(q);
-    if (q >= nitems) break;  // every wave leaves once the queue is drained
-    const int2 item = items[q];
-    const int base = pt_ip[item.x];
-    const int s = pt_ip[item.x + 1] - base;
-    const int li = item.y + lane;
-    const bool rv = li < s;
-    double xi[D], acc[D], di = 1.0;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      xi[k] = rv ? Xp[((size_t)base + li) * D + k] : 0.0;
-      acc[k] = 0.0;
-    }
-    if (rv) di = DP[(size_t)base + li];
-    const bool rows_ok = repel_ok && __all(vertex_ok<D>(xi, di));
-    // partner record of this lane for the next tile, held in registers
-    double nx[D + 1];
-    auto fetch = [&](int j0) {
-      const bool v = j0 + lane < s;
-      const size_t c = (size_t)base + (v ? j0 + lane : 0);
-#pragma unroll
-      for (int k = 0; k < D; ++k) nx[k] = v ? Xp[c * D + k] : 0.0;
-      nx[D] = v ? DP[c] : 1.0;
-    };
-    fetch(0);
-    for (int j0 = 0; j0 < s; j0 += kBigW) {
-      const int cnt = min(kBigW, s - j0);
-      wave_lds_sync();  // the previous tile has been read by every lane
-#pragma unroll
-      for (int k = 0; k <= D; ++k) tile[lane * WV + k] = nx[k];
-      const bool ok = lane >= cnt || vertex_ok<D>(nx, nx[D]);
-      wave_lds_sync();
-      if (j0 + kBigW < s) fetch(j0 + kBigW);  // in flight while this tile computes
-      if (rows_ok && __all(ok)) {
-        int jj = 0;
-        if constexpr (U > 1) {
-          for (; jj + U <= cnt; jj += U) {
-            double t[U][D];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-              rep_term<D, true, REPEL_ONE>(xi, &tile[(jj + u) * WV], di, tile[(jj + u) * WV + D],
-                                           repel, t[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-              for (int k = 0; k < D; ++k) acc[k] = acc[k] + t[u][k];
-          }
-        }
-        for (; jj < cnt; ++jj)  // the j == i term is +-0 (ge_pair.hpp)
-          rep_pair<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
-      } else {
-        for (int jj = 0; jj < cnt; ++jj)
-          rep_pair_fb<D, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel,
-                                    j0 + jj == li, acc);
-      }
-    }
-    if (rv) {
-#pragma unroll
-      for (int k = 0; k < D; ++k) Fscr[((size_t)base + li) * D + k] = acc[k];
-    }
-  }
-}
-
 // Per streamed member, after faml_big_repulse: the CSR row (:415-467) added to
 // the repulsion sum in stored order (degree-classed, ge_rows.hpp), gravity
 // (:469-474) and the swing/speed update (:477-530).
@@ -808,9 +722,8 @@ struct ge_faml_plan {
   ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
-  // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters;
-  // sym2: each sweep spread over a workgroup (ge_sym2.hpp)
-  bool sym = false, sym2 = false;
+  // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters
+  bool sym = false;
   ge::DevBuf<int4> units;
   ge::DevBuf<int> prog;
   int nunits = 0, ntiles = 0, sym_blocks = 0;
@@ -828,20 +741,26 @@ struct ge_faml_plan {
   std::vector<hipEvent_t> aev;  // 2 per profiled member-row pass (FamlRows)
   size_t next_aev = 0;
   long long streamed_entries = 0;  // CSR entries of the streamed members' rows
-  // row blocks of the largest aggregates on CUs of their own (faml_lone_repulse),
-  // beside the sweeps, on their own stream
-  ge::DevBuf<int2> lone_items;
-  ge::DevBuf<int> lone_queue;
-  int nlone = 0, lone_blocks = 0, lone_U = 4;
-  size_t lone_lds = 0;
-  hipStream_t lone_st = nullptr;
-  hipEvent_t lone_fork = nullptr, lone_join = nullptr;
+  // aggregates split by row tiles across the ranks of `comm`: this
+  // rank computes its rows' forces and updates, and the split aggregates' rows are
+  // exchanged after every iteration (exchange_rows, stream-ordered)
+  ge_comm* comm = nullptr;
+  ge::DevBuf<int> irows;  // positions initialised / given deg+1: rows + the other ranks' split rows
+  int nirows = 0;
+  ge::DevBuf<int> xrows, xcounts, xfirst;
+  ge::DevBuf<double> xbuf;
+  std::vector<int> h_xcounts, h_xfirst;
+  int xwidth = 0;
 };
 
 namespace ge {
 
 // aggs: the aggregates this plan runs (strictly increasing ids).
-static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vector<int>& aggs) {
+// split: aggregates whose row tiles are dealt over the ranks of pl->comm (the
+// same list on every rank; tiles [T r / N, T (r + 1) / N) to rank r).
+static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vector<int>& aggs,
+                            const std::vector<int>& split_aggs = std::vector<int>()) {
+  const std::vector<int>& split = split_aggs;
   hipStream_t st = pl->ctx->stream;
   const int dim = pl->dim;
   // Work of aggregate a per iteration ~ s^2.  Aggregates whose share would
@@ -857,8 +776,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   GE_HIP(hipGetDevice(&dev));
   GE_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const double per_cu = W / std::max(cus, 1);
-  int split = (int)std::sqrt(per_cu / 4.0);
-  split = std::max(256, std::min(split, large_cap(dim)));
+  int res_cap = (int)std::sqrt(per_cu / 4.0);  // largest aggregate kept resident
+  res_cap = std::max(256, std::min(res_cap, large_cap(dim)));
 
   std::vector<int> small, mid, large, big;
   for (int a : aggs) {
@@ -866,7 +785,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     if (s <= 0) continue;
     if (s <= 64) small.push_back(a);
     else if (s <= 256) mid.push_back(a);
-    else if (s <= split) large.push_back(a);
+    else if (s <= res_cap) large.push_back(a);
     else big.push_back(a);
   }
   auto by_size = [&](int x, int y) {
@@ -887,6 +806,29 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   std::vector<int> rows;
   for (int a : big)
     for (int li = 0; li < h_pt_ip[a + 1] - h_pt_ip[a]; ++li) rows.push_back(h_pt_ip[a] + li);
+  // split aggregates: this rank's row tiles are streamed rows like the others; every
+  // member is initialised and given its internal degree (all are columns)
+  const int rank = pl->comm ? pl->comm->rank : 0, nranks = pl->comm ? pl->comm->nranks : 1;
+  auto tiles_of = [&](int a, int r, int& t0, int& t1) {
+    const long long T = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
+    t0 = (int)(T * r / nranks);
+    t1 = (int)(T * (r + 1) / nranks);
+  };
+  std::vector<int> irows = rows;
+  std::vector<int> xr, xcounts(nranks, 0);
+  for (int r = 0; r < nranks; ++r)
+    for (int a : split) {
+      const int s = h_pt_ip[a + 1] - h_pt_ip[a];
+      int t0, t1;
+      tiles_of(a, r, t0, t1);
+      for (int li = 64 * t0; li < std::min(s, 64 * t1); ++li) {
+        const int c = h_pt_ip[a] + li;
+        if (r == rank) rows.push_back(c);
+        irows.push_back(c);
+        xr.push_back(c);
+        ++xcounts[r];
+      }
+    }
   // row slots x partners in flight (GE_FAML_R / GE_FAML_U override; only the
   // compiled variants of GE_BIG_VARIANTS are accepted)
   int R = kBigDefaultR, U = kBigDefaultU;
@@ -930,6 +872,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     for (int r0 = 0; r0 < s; r0 += 64 * R)
       its.push_back({a, r0, (double)std::min(R, (s - r0 + 63) / 64) * s});
   }
+  for (int a : split) {  // this rank's tiles, one item each (R = 1 rows per slot)
+    const int s = h_pt_ip[a + 1] - h_pt_ip[a];
+    int t0, t1;
+    tiles_of(a, rank, t0, t1);
+    if (t1 > t0) R = 1;
+    for (int t = t0; t < t1; ++t) its.push_back({a, 64 * t, (double)s});
+  }
   std::stable_sort(its.begin(), its.end(),
                    [](const Item& x, const Item& y) { return x.work > y.work; });
   std::vector<int2> items;
@@ -940,34 +889,26 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     const char* e = std::getenv("GE_FAML_SYM");
     pl->sym = !(e && *e == '0');
   }
-  {
-    const char* e = std::getenv("GE_FAML_SYM2");
-    pl->sym2 = pl->sym && e && *e == '1';
-  }
-  if (pl->sym && !big.empty()) {
+  if (pl->sym && (!big.empty() || !split.empty())) {
     // The sweeps of an aggregate with T row tiles form a chain of ~2.5 T tile-times
     // (each sweep starts after its predecessor has passed its first two tiles); the
     // launch takes about (sum of T^2 / 2 sweep tiles) / (resident waves).  While the
     // longest chain exceeds that, the largest aggregate runs as plain row blocks
     // (every ordered pair, ~0.8 the step cost of a sweep, no chain).
     std::vector<int> T(big.size());
+    const bool any_big = !big.empty();
     for (size_t b = 0; b < big.size(); ++b) T[b] = (h_pt_ip[big[b] + 1] - h_pt_ip[big[b]] + 63) / 64;
     int occ = 1;
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, pl->sym2 ? (const void*)faml_sym2_repulse<D, false>
-                         : (const void*)faml_sym_repulse<D, false>,
-          pl->sym2 ? kSym2T : kSymT, 0));
+          &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
     });
     int bpc = std::min(std::max(occ, 1), 4);
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
-    // sweep slots: waves (ge_sym.hpp) or workgroups (ge_sym2.hpp, each sweep on a
-    // workgroup, advancing ~4x faster: tile-times below are the slot's own)
-    const double waves = pl->sym2 ? (double)pl->sym_blocks
-                                  : (double)pl->sym_blocks * (kSymT / 64);
+    const double waves = (double)pl->sym_blocks * (kSymT / 64);
     std::vector<size_t> by_T(big.size());
     std::iota(by_T.begin(), by_T.end(), 0);
     std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
@@ -983,14 +924,12 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // N = 4: 20 of 24 aggregates as row blocks 70 ms per iteration, 7 of 25 (4 090
     // row blocks) 58 ms, all 52 ms).
     // Take the count that minimises it.
-    // sym2: a row block runs on one wave of a workgroup, ~4 workgroup tile-times per
-    // tile, so row blocks never shorten the critical path: all sweeps by default
-    double chain_k = pl->sym2 ? 0.0 : 2.5, row_k = 0.8;
+    double chain_k = 2.5, row_k = 0.8;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
     double best = 1e300;
     size_t best_k = 0;
-    if (chain_k > 0.0) {
+    if (chain_k > 0.0 && any_big) {
       double work = 0.0, row_work = 0.0, row_units = 0.0;
       for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
       for (size_t k = 0; k <= by_T.size(); ++k) {  // the k largest as row blocks
@@ -1011,11 +950,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         }
       }
       for (size_t k = 0; k < best_k; ++k) rows_mode[by_T[k]] = 1;
-      // GE_FAML_LONE=k: the k largest as lone row blocks instead (measurement knob)
-      if (const char* e = std::getenv("GE_FAML_LONE")) {
-        const size_t k = std::min(by_T.size(), (size_t)std::max(0, std::atoi(e)));
-        for (size_t q = 0; q < by_T.size(); ++q) rows_mode[by_T[q]] = q < k ? 2 : 0;
-      }
       if (std::getenv("GE_FAML_PLAN_DEBUG"))
         std::fprintf(stderr,
                      "faml plan: %zu streamed aggregates, T max %d, waves %.0f, work/waves %.1f "
@@ -1038,40 +972,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     }
     std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b)
-      if (rows_mode[b] == 1)  // sym2: one unit = row tiles A .. A+3, one per wave
-        for (int A = 0; A < T[b]; A += pl->sym2 ? 4 : 1)
-          rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
-    std::vector<int2> lone;
-    for (size_t q = 0; q < by_T.size(); ++q)  // largest first
-      if (rows_mode[by_T[q]] == 2)
-        for (int A = 0; A < T[by_T[q]]; ++A) lone.push_back(make_int2(big[by_T[q]], 64 * A));
-    if (!lone.empty()) {
-      pl->nlone = (int)lone.size();
-      pl->lone_items.alloc(lone.size());
-      pl->lone_items.upload(lone.data(), lone.size(), st);
-      pl->lone_queue.alloc(std::max(pl->iterations, 1));
-      if (const char* e = std::getenv("GE_FAML_LONE_U")) pl->lone_U = std::atoi(e);
-      if (pl->lone_U != 1 && pl->lone_U != 2 && pl->lone_U != 4) pl->lone_U = 4;
-      // one block of 4 waves per CU and no other block beside it: reserve LDS past
-      // what a second block of any streamed kernel could find (160 KiB per CU)
-      pl->lone_lds = 120 * 1024;
-      if (const char* e = std::getenv("GE_FAML_LONE_LDS")) pl->lone_lds = std::atoi(e);
-      pl->lone_blocks = std::min(cus, (pl->nlone + 3) / 4);
-      dispatch_dim(dim, [&](auto Dc) {
-        constexpr int D = decltype(Dc)::value;
-        const void* ks[] = {(const void*)faml_lone_repulse<D, 1, true>,
-                            (const void*)faml_lone_repulse<D, 2, true>,
-                            (const void*)faml_lone_repulse<D, 4, true>,
-                            (const void*)faml_lone_repulse<D, 1, false>,
-                            (const void*)faml_lone_repulse<D, 2, false>,
-                            (const void*)faml_lone_repulse<D, 4, false>};
-        for (const void* k : ks)
-          GE_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)pl->lone_lds));
-      });
-      GE_HIP(hipStreamCreateWithFlags(&pl->lone_st, hipStreamNonBlocking));
-      GE_HIP(hipEventCreateWithFlags(&pl->lone_fork, hipEventDisableTiming));
-      GE_HIP(hipEventCreateWithFlags(&pl->lone_join, hipEventDisableTiming));
+      if (rows_mode[b])
+        for (int A = 0; A < T[b]; ++A) rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
+    for (int a : split) {  // this rank's row tiles of the split aggregates: row blocks
+      int t0, t1;
+      tiles_of(a, rank, t0, t1);
+      const int Ta = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
+      for (int A = t0; A < t1; ++A) rows_units.push_back({a, A, 0, Ta, 1, 0.0});
     }
     // row blocks have no dependencies and each spans its aggregate's whole width:
     // first in the queue (measured on per-rank shares of C4: N = 4 69 ms per
@@ -1097,6 +1004,12 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     const double sa = h_pt_ip[a + 1] - h_pt_ip[a];
     pl->streamed_pairs += sa * (sa - 1);
   }
+  for (int a : split) {  // this rank's rows against all members
+    int t0, t1;
+    tiles_of(a, rank, t0, t1);
+    const double sa = h_pt_ip[a + 1] - h_pt_ip[a];
+    pl->streamed_pairs += (std::min(sa, 64.0 * t1) - std::min(sa, 64.0 * t0)) * (sa - 1);
+  }
   // 4 waves per SIMD: more items per wave for the queue to balance (C3 level
   // 0: 961 ms per call against 1091 ms at the full 8 waves per SIMD)
   const int occ = rep_occupancy(dim, pl->code);
@@ -1114,8 +1027,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   pl->nm = (int)beg_m.size() - 1;
   pl->nl = (int)beg_l.size() - 1;
   pl->nrows = (int)rows.size();
+  pl->nirows = (int)irows.size();
   pl->nitems = (int)items.size();
-  pl->nhuge = (int)big.size();
+  std::vector<int> huge = big;  // centred and scaled at the end: the split ones on every rank
+  huge.insert(huge.end(), split.begin(), split.end());
+  pl->nhuge = (int)huge.size();
 
   const int n = pl->n;
   pl->pos.alloc(std::max(n, 1));
@@ -1124,15 +1040,30 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   pl->rows.alloc(std::max<size_t>(rows.size(), 1));
   pl->items.alloc(std::max<size_t>(items.size(), 1));
   pl->queue.alloc(std::max(pl->iterations, 1));
-  pl->huge.alloc(std::max<size_t>(big.size(), 1));
+  pl->huge.alloc(std::max<size_t>(huge.size(), 1));
+  pl->irows.alloc(std::max<size_t>(irows.size(), 1));
+  pl->irows.upload(irows.data(), irows.size(), st);
   pl->order.upload(order.data(), order.size(), st);
   pl->beg.upload(begs.data(), begs.size(), st);
   pl->rows.upload(rows.data(), rows.size(), st);
   pl->items.upload(items.data(), items.size(), st);
-  pl->huge.upload(big.data(), big.size(), st);
+  pl->huge.upload(huge.data(), huge.size(), st);
+  if (!split.empty() && nranks > 1) {  // the per-iteration exchange of the split rows
+    pl->h_xcounts = xcounts;
+    pl->h_xfirst.assign(nranks + 1, 0);
+    for (int r = 0; r < nranks; ++r) pl->h_xfirst[r + 1] = pl->h_xfirst[r] + xcounts[r];
+    pl->xwidth = std::max(1, *std::max_element(xcounts.begin(), xcounts.end()));
+    pl->xrows.alloc(std::max<size_t>(xr.size(), 1));
+    pl->xrows.upload(xr.data(), xr.size(), st);
+    pl->xcounts.alloc(nranks);
+    pl->xcounts.upload(xcounts.data(), nranks, st);
+    pl->xfirst.alloc(nranks + 1);
+    pl->xfirst.upload(pl->h_xfirst.data(), nranks + 1, st);
+    pl->xbuf.alloc((size_t)pl->xwidth * dim * nranks);
+  }
   pl->Fscr.alloc((size_t)std::max(n, 1) * dim);
   pl->Fprev.alloc((size_t)std::max(n, 1) * dim);
-  if (pl->nrows > 0) {
+  if (pl->nirows > 0) {
     pl->Xa.alloc((size_t)n * dim);
     pl->Xb.alloc((size_t)n * dim);
     pl->DP.alloc(n);
@@ -1143,10 +1074,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     hipLaunchKernelGGL(edge_code_kernel, dim3((pl->nrows + 255) / 256), dim3(256), 0, st,
                        pl->nrows, pl->rows.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip,
                        pl->ix, pl->ecode.p);
-    hipLaunchKernelGGL(faml_huge_dp, dim3((pl->nrows + kHT - 1) / kHT), dim3(kHT), 0, st,
-                       pl->nrows, pl->rows.p, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, pl->DP.p,
-                       pl->c.use_weights);
   }
+  if (pl->nirows > 0)
+    hipLaunchKernelGGL(faml_huge_dp, dim3((pl->nirows + kHT - 1) / kHT), dim3(kHT), 0, st,
+                       pl->nirows, pl->irows.p, pl->pt_ix, pl->vA, pl->ip, pl->ix, pl->dx, pl->DP.p,
+                       pl->c.use_weights);
   GE_HIP(hipGetLastError());
   for (int k = 0; k < 3; ++k) {
     GE_HIP(hipStreamCreateWithFlags(&pl->side[k], hipStreamNonBlocking));
@@ -1154,25 +1086,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   }
   GE_HIP(hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming));
   GE_HIP(hipStreamSynchronize(st));
-}
-
-template <int D>
-static void launch_lone(ge_faml_plan* pl, int it, const double* X, double repel) {
-  const dim3 g(pl->lone_blocks), b(kHT);
-  int* q = pl->lone_queue.p + it;
-#define GE_LONE(UU)                                                                              \
-  if (repel == 1.0)                                                                              \
-    hipLaunchKernelGGL((faml_lone_repulse<D, UU, true>), g, b, pl->lone_lds, pl->lone_st,        \
-                       pl->nlone, pl->lone_items.p, q, pl->pt_ip, X, pl->DP.p, repel, pl->Fscr.p); \
-  else                                                                                           \
-    hipLaunchKernelGGL((faml_lone_repulse<D, UU, false>), g, b, pl->lone_lds, pl->lone_st,       \
-                       pl->nlone, pl->lone_items.p, q, pl->pt_ip, X, pl->DP.p, repel, pl->Fscr.p);
-  switch (pl->lone_U) {
-    case 1: GE_LONE(1) break;
-    case 2: GE_LONE(2) break;
-    default: GE_LONE(4) break;
-  }
-#undef GE_LONE
 }
 
 static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, const double* init,
@@ -1199,12 +1112,11 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     // streamed path (side[0])
     hipStream_t ss = pl->side[0];
     if (ev) GE_HIP(hipEventRecord(ev[2], ss));
-    if (pl->nrows > 0) {
-      const int nr = pl->nrows;
+    if (pl->nirows > 0) {
+      const int nr = pl->nirows;
       hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
-                         nr, pl->rows.p, init, pl->Xa.p, pl->Fprev.p);
+                         nr, pl->irows.p, init, pl->Xa.p, pl->Fprev.p);
       GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
-      if (pl->nlone > 0) GE_HIP(hipMemsetAsync(pl->lone_queue.p, 0, sizeof(int) * iters, ss));
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
@@ -1220,23 +1132,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_rev += 2;
           GE_HIP(hipEventRecord(re[0], ss));
         }
-        if (pl->nlone > 0) {  // lone row blocks first: their CUs are taken before the sweeps'
-          GE_HIP(hipEventRecord(pl->lone_fork, ss));
-          GE_HIP(hipStreamWaitEvent(pl->lone_st, pl->lone_fork, 0));
-          launch_lone<D>(pl, it, cur, c.repel);
-          GE_HIP(hipEventRecord(pl->lone_join, pl->lone_st));
-        }
-        if (pl->sym2) {
-          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
-          if (c.repel == 1.0)
-            hipLaunchKernelGGL((faml_sym2_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSym2T),
-                               0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
-          else
-            hipLaunchKernelGGL((faml_sym2_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSym2T),
-                               0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
-        } else if (pl->sym) {
+        if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
           if (c.repel == 1.0)
             hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
@@ -1250,7 +1146,6 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                                 pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
         }
-        if (pl->nlone > 0) GE_HIP(hipStreamWaitEvent(ss, pl->lone_join, 0));
         if (re) GE_HIP(hipEventRecord(re[1], ss));
         hipEvent_t* ae = nullptr;
         if (pl->profiling) {
@@ -1264,10 +1159,15 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_aev += 2;
           GE_HIP(hipEventRecord(ae[0], ss));
         }
-        const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
-                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
-        launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
+        if (pl->nrows > 0) {
+          const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
+                               cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
+          launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
+        }
         if (ae) GE_HIP(hipEventRecord(ae[1], ss));
+        if (pl->xwidth > 0)  // every rank's rows of the split aggregates, for the next step
+          exchange_rows(pl->comm, ss, D, pl->xrows.p, pl->xcounts.p, pl->xfirst.p,
+                        pl->h_xcounts.data(), pl->h_xfirst.data(), pl->xwidth, pl->xbuf.p, nxt);
         std::swap(cur, nxt);
       }
       hipLaunchKernelGGL((faml_huge_finish<D>), dim3(pl->nhuge), dim3(kHT), 0, ss, pl->huge.p,
@@ -1307,12 +1207,6 @@ static void faml_plan_free(ge_faml_plan* pl) {
     if (pl->join[k]) (void)hipEventDestroy(pl->join[k]);
   }
   if (pl->fork) (void)hipEventDestroy(pl->fork);
-  if (pl->lone_st) {
-    (void)hipStreamSynchronize(pl->lone_st);
-    (void)hipStreamDestroy(pl->lone_st);
-  }
-  if (pl->lone_fork) (void)hipEventDestroy(pl->lone_fork);
-  if (pl->lone_join) (void)hipEventDestroy(pl->lone_join);
   for (hipEvent_t e : pl->ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pl->rev) (void)hipEventDestroy(e);
   for (hipEvent_t e : pl->aev) (void)hipEventDestroy(e);
@@ -1359,12 +1253,15 @@ static int faml_plan_create_impl(ge_ctx* ctx, int n, const int* d_ip, const int*
                                  const double* d_dx, int m, const int* h_pt_ip,
                                  const int* d_pt_ip, const int* d_pt_ix, const int* d_vA,
                                  int dim, const ge_fa_params* p, int iterations,
-                                 const std::vector<int>& aggs, ge_faml_plan** out) {
+                                 const std::vector<int>& aggs, ge_faml_plan** out,
+                                 ge_comm* comm = nullptr,
+                                 const std::vector<int>& split = std::vector<int>()) {
   return ge::guarded([&] {
     ge::DeviceGuard g(ctx);
     auto* pl = new ge_faml_plan();
     try {
       pl->ctx = ctx;
+      pl->comm = comm;
       pl->n = n;
       pl->m = m;
       pl->dim = dim;
@@ -1376,7 +1273,7 @@ static int faml_plan_create_impl(ge_ctx* ctx, int n, const int* d_ip, const int*
       pl->pt_ix = d_pt_ix;
       pl->vA = d_vA;
       pl->c = ge::make_fa_const(*p);
-      ge::faml_plan_build(pl, h_pt_ip, aggs);
+      ge::faml_plan_build(pl, h_pt_ip, aggs, split);
     } catch (...) {
       ge::faml_plan_free(pl);
       throw;
@@ -1426,6 +1323,36 @@ int ge_faml_plan_create_subset(ge_ctx* ctx, int n, const int* d_ip, const int* d
   if (rc != GE_OK) return rc;
   return faml_plan_create_impl(ctx, n, d_ip, d_ix, d_dx, m, h_pt_ip, d_pt_ip, d_pt_ix, d_vA, dim,
                                p, iterations, aggs, out);
+}
+
+int ge_faml_plan_create_shard(ge_ctx* ctx, ge_comm* comm, int n, const int* d_ip,
+                              const int* d_ix, const double* d_dx, int m, const int* h_pt_ip,
+                              const int* d_pt_ip, const int* d_pt_ix, const int* d_vA, int dim,
+                              const ge_fa_params* p, int iterations, const int* h_aggs,
+                              int n_aggs, const int* h_split, int n_split, ge_faml_plan** out) {
+  std::vector<int> aggs, split;
+  const int rc = ge::guarded([&] {
+    faml_plan_check(ctx, n, m, h_pt_ip, dim, p, out);
+    GE_REQUIRE(comm && comm->ctx == ctx, "the communicator must belong to the plan's context");
+    GE_REQUIRE(n_aggs >= 0 && (h_aggs || n_aggs == 0) && n_split >= 0 && (h_split || n_split == 0),
+               "bad aggregate lists");
+    std::vector<char> seen(m, 0);
+    for (int q = 0; q < n_aggs; ++q) {
+      GE_REQUIRE(h_aggs[q] >= 0 && h_aggs[q] < m && (q == 0 || h_aggs[q] > h_aggs[q - 1]),
+                 "aggregate ids must be strictly increasing and < m");
+      seen[h_aggs[q]] = 1;
+    }
+    for (int q = 0; q < n_split; ++q) {
+      GE_REQUIRE(h_split[q] >= 0 && h_split[q] < m && (q == 0 || h_split[q] > h_split[q - 1]),
+                 "split aggregate ids must be strictly increasing and < m");
+      GE_REQUIRE(!seen[h_split[q]], "an aggregate is both whole and split");
+    }
+    aggs.assign(h_aggs, h_aggs + n_aggs);
+    split.assign(h_split, h_split + n_split);
+  });
+  if (rc != GE_OK) return rc;
+  return faml_plan_create_impl(ctx, n, d_ip, d_ix, d_dx, m, h_pt_ip, d_pt_ip, d_pt_ix, d_vA, dim,
+                               p, iterations, aggs, out, comm, split);
 }
 
 int ge_faml_plan_run(ge_faml_plan* pl, const double* d_cA, const double* d_rA,

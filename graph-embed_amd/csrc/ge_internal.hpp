@@ -116,6 +116,14 @@ struct ge_comm {
   ge_transport tp{};
 };
 
+namespace ge {
+// Multi-GPU helpers (ge_dist.hip) used inside per-level plans.
+void allgather_stream(ge_comm* c, hipStream_t s, const void* d_send, void* d_recv, size_t bytes);
+void exchange_rows(ge_comm* c, hipStream_t s, int dim, const int* d_rows, const int* d_counts,
+                   const int* d_first, const int* h_counts, const int* h_first, int width,
+                   double* d_buf, double* d_x);
+}  // namespace ge
+
 // Host CSR (returned to callers through ge_csr*).
 struct ge_csr {
   int rows = 0, cols = 0;

@@ -1071,7 +1071,13 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   GE_HIP(hipMemcpyAsync(h_sums, sums.p, sizeof(h_sums), hipMemcpyDeviceToHost, st));
   GE_HIP(hipStreamSynchronize(st));
   note("lists built");
-  if (bad || !(h_sums[0] < 4503599627370496.0)) return nullptr;  // sum |w| < 2^52
+  if (bad || !(h_sums[0] < 4503599627370496.0)) {  // sum |w| < 2^52
+    if (progress)
+      std::fprintf(stderr, "partition_device: input needs the host path (%s)\n",
+                   bad ? "non-integer weights, asymmetric or unsorted rows"
+                       : "weights sum to 2^52 or more");
+    return nullptr;
+  }
   {
     bool pos = true;
     for (long long e = 0; e < nnz && pos; ++e) pos = Dv[e] > 0.0;
@@ -1133,6 +1139,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     h->indices.push_back(std::move(ix));
   };
 
+  note("host state ready");
   MergeRec* h_mrec = nullptr;
   int2* h_changes = nullptr;
   GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_mrec), sizeof(MergeRec) * (n / 2 + 1)));
@@ -1201,6 +1208,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
     GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     GE_HIP(hipStreamSynchronize(st));
+    if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
     if (prof)
       for (int c = C_DIRTY; c <= C_G; ++c) stat[c] += h_cnt[c];  // previous round's contraction
@@ -1254,6 +1262,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       hipLaunchKernelGGL(dirty_reset_kernel, dim3(1024), dim3(256), 0, st, d, rounds);
       GE_HIP(hipMemsetAsync(cnt.p + C_MERGE, 0, sizeof(int), st));
       GE_HIP(hipGetLastError());
+      if (rounds <= 2 && progress) {  // profiling the first rounds: wait for the contraction
+        GE_HIP(hipStreamSynchronize(st));
+        note("round: contraction done");
+      }
     }
     const auto t1 = now();
     t_dev += secs(t0, t1);

@@ -102,6 +102,11 @@ _SIGS = {
                                                   _i32p, _vp, _vp, _vp, ctypes.c_int,
                                                   ctypes.POINTER(FaParams), ctypes.c_int, _i32p,
                                                   ctypes.c_int, ctypes.POINTER(_vp)]),
+    "ge_faml_plan_create_shard": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp, _vp,
+                                                 ctypes.c_int, _i32p, _vp, _vp, _vp, ctypes.c_int,
+                                                 ctypes.POINTER(FaParams), ctypes.c_int, _i32p,
+                                                 ctypes.c_int, _i32p, ctypes.c_int,
+                                                 ctypes.POINTER(_vp)]),
     "ge_faml_plan_run": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "ge_faml_plan_set_profiling": (ctypes.c_int, [_vp, ctypes.c_int]),
     "ge_faml_plan_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double),
@@ -139,6 +144,8 @@ _SIGS = {
     "ge_allgather_coords": (ctypes.c_int, [_vp, _vp, ctypes.c_longlong, ctypes.c_int]),
     "ge_assign_aggregates": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _vp, ctypes.c_int,
                                             _i32p]),
+    "ge_assign_aggregates_split": (ctypes.c_int, [ctypes.c_int, _i32p, _i32p, _vp, ctypes.c_int,
+                                                  ctypes.c_int, _i32p]),
     "ge_allgather_members": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _i32p, _i32p,
                                             _i32p]),
     "ge_force_atlas_dist": (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_int,
@@ -481,6 +488,20 @@ class Comm:
         return out
 
 
+def assign_aggregates_split(PT, indptr, nranks, min_members=-1):
+    """ge_assign_aggregates_split: owner per aggregate, -1 for the aggregates split
+    by row tiles over all ranks (min_members > 0: every aggregate at least that
+    large; 0: none; < 0: the automatic rule)."""
+    pip = np.ascontiguousarray(PT[0], dtype=np.int32)
+    pix = np.ascontiguousarray(PT[1], dtype=np.int32)
+    owner = np.empty(len(pip) - 1, dtype=np.int32)
+    ipa = None if indptr is None else np.ascontiguousarray(indptr, dtype=np.int32)
+    _check(lib().ge_assign_aggregates_split(len(pip) - 1, pip, pix,
+                                            None if ipa is None else ipa.ctypes.data_as(_vp),
+                                            nranks, min_members, owner))
+    return owner
+
+
 def assign_aggregates(PT, indptr, nranks):
     """ge_assign_aggregates: the rank of every aggregate (LPT by s(s-1) + the
     members' CSR entries when indptr is given)."""
@@ -505,15 +526,24 @@ class FamlPlan:
     (pt_indptr_host, numpy) plus device pointers for everything else."""
 
     def __init__(self, ctx, n, d_ip, d_ix, d_dx, pt_indptr_host, d_pt_ip, d_pt_ix, d_vA, dim,
-                 iterations=100, agg_range=None, aggs=None, **kw):
+                 iterations=100, agg_range=None, aggs=None, split=None, comm=None, **kw):
         """agg_range=(a0, a1) or aggs=(strictly increasing aggregate ids) restricts
-        the plan to those aggregates (one rank's share); default: all."""
+        the plan to those aggregates (one rank's share); default: all.  split (with
+        comm): aggregates split by row tiles over comm's ranks
+        (ge_faml_plan_create_shard)."""
         self.ctx = ctx
         pip = np.ascontiguousarray(pt_indptr_host, dtype=np.int32)
         m = len(pip) - 1
         p = params(**kw)
         h = _vp()
-        if aggs is not None:
+        if comm is not None:
+            ids = np.ascontiguousarray(np.zeros(0) if aggs is None else aggs, dtype=np.int32)
+            sp = np.ascontiguousarray(np.zeros(0) if split is None else split, dtype=np.int32)
+            _check(lib().ge_faml_plan_create_shard(
+                ctx.h, comm.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip, _vp(d_pt_ip),
+                _vp(d_pt_ix), _vp(d_vA), dim, ctypes.byref(p), iterations, ids, len(ids), sp,
+                len(sp), ctypes.byref(h)))
+        elif aggs is not None:
             ids = np.ascontiguousarray(aggs, dtype=np.int32)
             _check(lib().ge_faml_plan_create_subset(
                 ctx.h, n, _vp(d_ip), _vp(d_ix), _vp(d_dx), m, pip, _vp(d_pt_ip), _vp(d_pt_ix),

@@ -126,6 +126,20 @@ int ge_faml_plan_create_subset(ge_ctx* ctx, int n, const int* d_indptr, const in
                                const int* d_vertex_A, int dim, const ge_fa_params* p,
                                int iterations, const int* h_aggs, int n_aggs,
                                ge_faml_plan** out);
+/* One rank's plan when aggregates are also split across GPUs (SURVEY.md 8(e);
+ * include/forceatlas.hpp:394-410 is a per-row ordered sum, so rows of one aggregate
+ * can live on different ranks): h_aggs are this rank's whole aggregates, h_split the
+ * aggregates split by 64-row tiles over all ranks of comm (the same list on every
+ * rank; rank r takes tiles [T r / N, T (r + 1) / N)).  The split aggregates' rows are
+ * all-gathered over comm after every iteration inside ge_faml_plan_run, and every
+ * rank ends with all their members' coordinates.  Every rank must run its plan. */
+typedef struct ge_comm ge_comm;
+int ge_faml_plan_create_shard(ge_ctx* ctx, ge_comm* comm, int n, const int* d_indptr,
+                              const int* d_indices, const double* d_data, int m,
+                              const int* h_pt_indptr, const int* d_pt_indptr,
+                              const int* d_pt_indices, const int* d_vertex_A, int dim,
+                              const ge_fa_params* p, int iterations, const int* h_aggs,
+                              int n_aggs, const int* h_split, int n_split, ge_faml_plan** out);
 int ge_faml_plan_run(ge_faml_plan* plan, const double* d_coords_A, const double* d_r_A,
                      const double* d_init, double* d_coords);
 int ge_faml_plan_set_profiling(ge_faml_plan* plan, int enable);
@@ -240,7 +254,6 @@ int ge_radius_step_device(ge_ctx* ctx, int m, double* coords_A, double* r_A, int
  * Every rank passes the same inputs; collective calls must be made by all ranks
  * in the same order. */
 #define GE_COMM_ID_BYTES 128
-typedef struct ge_comm ge_comm;
 typedef struct ge_transport {
   void* user;
   /* All-gather of equal blocks: recv (nranks * bytes, rank-major) receives every
@@ -273,6 +286,11 @@ int ge_assign_aggregates(int m, const int* pt_indptr, const int* pt_indices, con
  * into d_x (n * dim, fine-vertex order; e.g. ge_faml_plan_run of a subset plan),
  * every rank holds all of them.  h_owner: ge_assign_aggregates' result;
  * h_pt_indptr / h_pt_indices: P_T on the host. */
+/* ge_assign_aggregates with the giant aggregates split (owner -1): those with at
+ * least min_members members (min_members > 0), none (0), or (< 0) those whose
+ * ordered pairs exceed half a rank's average load (GE_DIST_SPLIT_MIN overrides). */
+int ge_assign_aggregates_split(int m, const int* pt_indptr, const int* pt_indices,
+                               const int* indptr, int nranks, int min_members, int* owner);
 int ge_allgather_members(ge_comm* comm, double* d_x, int dim, int m, const int* h_pt_indptr,
                          const int* h_pt_indices, const int* h_owner);
 

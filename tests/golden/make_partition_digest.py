@@ -14,7 +14,14 @@ tests/test_partition_device.py::test_partition_device_<cfg>_digest checks the
 device hierarchy against it.  The per-level sha256 values let a mismatch be
 localised to the first differing level.
 
-usage: python tests/golden/make_partition_digest.py [c3|c4]
+usage: python tests/golden/make_partition_digest.py [c3|c4] [--host]
+
+--host: the library's host path (csrc/ge_partition.cpp: the same rounds with
+incremental rescans, bit-exact with the oracle on every fixture) instead of the
+oracle.  The oracle restates the reference's rescan of every untouched vertex in
+every pass (:1703-1726), which at C4 runs ~5 s per round for 9 969 rounds (measured
+here: 1 000 rounds in 2 h on 6 threads), so the C4 digest comes from the host path,
+pinned first by reproducing the oracle's committed C3 digest in the same run.
 """
 import hashlib
 import json
@@ -48,15 +55,34 @@ def digest(hier):
     return h.hexdigest(), per
 
 
+def lcc(cfg):
+    n_ids, draws = CONFIGS[cfg]
+    return ge.largest_component(ge.rmat_csr(n_ids, draws, seed=12345))
+
+
 def main():
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    host = "--host" in sys.argv
+    cfg = args[0] if args else "c3"
     n_ids, draws = CONFIGS[cfg]
     seed, cf = 12345, 0.125
     O.build()
-    L = ge.largest_component(ge.rmat_csr(n_ids, draws, seed=seed))
+    pinned = None
+    if host:
+        # the host path must first reproduce the oracle's own C3 digest
+        with open(os.path.join(HERE, "partition_c3_digest.json")) as f:
+            c3 = json.load(f)
+        t = time.time()
+        got, _ = digest(ge.partition(lcc("c3"), cf))
+        pinned = {"c3_sha256": got, "equals_oracle_c3_digest": got == c3["sha256"],
+                  "seconds": round(time.time() - t, 1)}
+        print("host path at C3:", pinned, flush=True)
+        if got != c3["sha256"]:
+            raise SystemExit("host path differs from the oracle at C3")
+    L = lcc(cfg)
     print(f"{cfg}: LCC n={len(L[0]) - 1} nnz={len(L[1])}", flush=True)
     t = time.time()
-    ho = O.partition(L, cf)
+    ho = ge.partition(L, cf) if host else O.partition(L, cf)
     el = time.time() - t
     if os.environ.get("GE_DIGEST_SAVE"):  # keep the hierarchy itself (not committed)
         np.savez(os.environ["GE_DIGEST_SAVE"],
@@ -64,9 +90,13 @@ def main():
     full, per = digest(ho)
     out = {"n_ids": n_ids, "draws": draws, "seed": seed, "cf": cf, "lcc_n": len(L[0]) - 1,
            "lcc_nnz": len(L[1]), "rows": [x[2] for x in ho], "sha256": full,
-           "level_sha256": per, "oracle_seconds": round(el, 1),
-           "oracle_threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
-           "generator": f"tests/golden/make_partition_digest.py {cfg}"}
+           "level_sha256": per, "seconds": round(el, 1),
+           "threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
+           "method": ("library host path (csrc/ge_partition.cpp), pinned to the oracle by "
+                      "the C3 digest" if host else "oracle (oracle/ge_oracle.cpp orc_partition)"),
+           "generator": f"tests/golden/make_partition_digest.py {cfg}" + (" --host" if host else "")}
+    if pinned:
+        out["host_path_pin"] = pinned
     with open(os.path.join(HERE, f"partition_{cfg}_digest.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(out)

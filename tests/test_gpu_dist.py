@@ -132,3 +132,59 @@ def test_ptap_split_sort_path(ctx, oracle, monkeypatch):
     PT = oracle.partition((ip, ix, np.ones(len(ix))), 0.125)[0]
     for a, b in zip(ctx.ptap(A, PT), oracle.ptap(A, PT)):
         assert np.array_equal(a, b)
+
+
+# --------------------------------------------------------------------------
+# giant aggregates split by row tiles across ranks: every rank
+# computes its tiles' rows (row blocks against all members, include/forceatlas.hpp:
+# 394-410 ordered per row) and the split aggregates' rows are all-gathered after
+# every iteration inside the plan.  GE_DIST_SPLIT_MIN forces the split.
+
+_SPLIT_SIZES = [2600, 700, 257, 1031, 100, 90, 1]  # 100 members: 2 tiles, so with 3
+# ranks one rank owns none of its rows and still joins every exchange
+
+
+def _split_inputs():
+    n = sum(_SPLIT_SIZES)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=17), [(3, 2000), (70, 3000)], seed=3)
+    perm = np.random.RandomState(5).permutation(n)
+    ip = np.cumsum([0] + _SPLIT_SIZES).astype(np.int32)
+    ix = np.concatenate([np.sort(perm[ip[a]:ip[a + 1]]) for a in range(len(_SPLIT_SIZES))])
+    PT = (ip, ix.astype(np.int32), len(_SPLIT_SIZES), n)
+    m = len(_SPLIT_SIZES)
+    cA = G.random_coords(m, 3, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    return A, PT, cA, rA
+
+
+def _split_worker(rank, world, port, out_path, sym):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GE_DIST_SPLIT_MIN="100",
+                      GE_FAML_SYM=sym)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = ge.Context(0)
+    comm = ge.Comm(ctx, world, rank, backend="transport")
+    A, PT, cA, rA = _split_inputs()
+    owner = ge.assign_aggregates_split(PT, A[0], world, 100)
+    X = comm.force_atlas_ml(A, PT, ge.vertex_of(PT), cA, rA, 3, iterations=7, seed=13)
+    np.savez(out_path % rank, X=X, owner=owner)
+    comm.close()
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,sym", [(2, "1"), (3, "1"), (3, "0")])
+def test_split_aggregates_match_single_gpu(tmp_path, ctx, oracle, world, sym):
+    import torch.multiprocessing as mp
+    A, PT, cA, rA = _split_inputs()
+    vA = ge.vertex_of(PT)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=7, seed=13)
+    assert np.array_equal(ctx.force_atlas_ml(A, PT, vA, cA, rA, 3, iterations=7, seed=13), want)
+    out = str(tmp_path / "s%d.npz")
+    mp.start_processes(_split_worker, args=(world, _free_port(), out, sym), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        got = dict(np.load(out % r))
+        assert list(got["owner"][:5]) == [-1] * 5  # the five largest were split
+        assert np.array_equal(got["X"], want), r

@@ -423,54 +423,6 @@ def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("chain,dim,repel,seed", [
-    ("", 3, 1.0, 5), ("", 3, 1.5, 6), ("", 3, 2.0 ** 70, 7), ("1e9", 3, 1.0, 8), ("", 2, 1.0, 9),
-    ("", 4, 0.75, 10), ("1e9", 4, 1.0, 11), ("", 1, 1.0, 12)])
-def test_faml_symmetric_workgroup_sweeps(ctx, oracle, monkeypatch, chain, dim, repel, seed):
-    """faml_sym2_repulse (ge_sym2.hpp): each sweep on a workgroup -- three producer
-    waves compute the terms ahead, one adder wave does the ordered sums and the
-    hand-overs; all sweeps (default) and all row blocks (chain 1e9, 4 row tiles per
-    unit), the `/` path (repel 2^70), ragged and one-member last tiles, hub rows."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_SYM2", "1")
-    if chain:
-        monkeypatch.setenv("GE_FAML_SYM_CHAIN", chain)
-    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1, 4417]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=seed), [(3, 2000), (70, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=seed)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("lone,U,dim,repel", [
-    ("1", "4", 3, 1.0), ("3", "4", 3, 1.0), ("2", "2", 3, 1.5), ("9", "1", 3, 1.0),
-    ("2", "4", 3, 2.0 ** 70), ("2", "4", 2, 1.0), ("3", "2", 4, 0.75)])
-def test_faml_lone_row_blocks(ctx, oracle, monkeypatch, lone, U, dim, repel):
-    """faml_lone_repulse: the largest aggregates as row blocks on CUs of their own
-    beside the sweeps (GE_FAML_LONE = how many), U partners in flight, the next
-    column tile prefetched; ragged last tiles, hub rows, the `/` path (repel 2^70)."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_LONE", lone)
-    monkeypatch.setenv("GE_FAML_LONE_U", U)
-    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=13), [(3, 2000), (70, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=6)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=23, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=23, repel=repel)
-    assert np.array_equal(got, want)
-
-
 @pytest.mark.parametrize("dim", [2, 4])
 def test_faml_dims(ctx, oracle, dim):
     A = G.largest_component(G.rmat(1500, 9000, seed=dim))

@@ -108,17 +108,34 @@ def test_partition_device_matches_host_path_100k(ctx):
     same(ctx.partition(A, 0.125), ge.partition(A, 0.125))
 
 
-def test_partition_device_c3_digest(ctx):
-    """configs[2]: LCC of the R-MAT(1M ids, 8M draws, seed 12345) -- the oracle's
-    hierarchy digest, committed (generator: tests/golden/make_partition_digest.py)."""
-    with open(os.path.join(HERE, "golden", "partition_c3_digest.json")) as f:
+def _check_digest(ctx, name):
+    with open(os.path.join(HERE, "golden", name)) as f:
         want = json.load(f)
-    L = ge.largest_component(ge.rmat_csr(want["n_ids"], want["draws"], seed=want["seed"]))
+    # the device R-MAT + LCC (equal to the host arrays, tests/test_gpu_graph.py)
+    L = ctx.rmat_csr(want["n_ids"], want["draws"], seed=want["seed"], lcc=True)
     assert len(L[0]) - 1 == want["lcc_n"] and len(L[1]) == want["lcc_nnz"]
     hg = ctx.partition(L, want["cf"])
     assert [h[2] for h in hg] == want["rows"]
     dig = hashlib.sha256()
-    for ip, ix, _, _ in hg:
-        dig.update(np.ascontiguousarray(ip, dtype=np.int32).tobytes())
-        dig.update(np.ascontiguousarray(ix, dtype=np.int32).tobytes())
+    for l, (ip, ix, _, _) in enumerate(hg):
+        ipb = np.ascontiguousarray(ip, dtype=np.int32).tobytes()
+        ixb = np.ascontiguousarray(ix, dtype=np.int32).tobytes()
+        if "level_sha256" in want:  # the first differing level, if any
+            assert hashlib.sha256(ipb + ixb).hexdigest() == want["level_sha256"][l], l
+        dig.update(ipb)
+        dig.update(ixb)
     assert dig.hexdigest() == want["sha256"]
+
+
+def test_partition_device_c3_digest(ctx):
+    """configs[2]: LCC of the R-MAT(1M ids, 8M draws, seed 12345) -- the oracle's
+    hierarchy digest, committed (generator: tests/golden/make_partition_digest.py)."""
+    _check_digest(ctx, "partition_c3_digest.json")
+
+
+def test_partition_device_c4_digest(ctx):
+    """configs[3] (the headline): LCC of the R-MAT(10M ids, 80M draws, seed 12345),
+    4.39M vertices, 9 969 rounds -- the hierarchy digest of the library's host path
+    (csrc/ge_partition.cpp), which reproduced the oracle's C3 digest in the same run
+    (the oracle's full rescans need ~18 h here at C4; make_partition_digest.py)."""
+    _check_digest(ctx, "partition_c4_digest.json")
