@@ -159,12 +159,70 @@ __global__ void lcc_copy_kernel(int n, const int* __restrict__ ip, const int* __
   }
 }
 
+// Library calls (hipcub sort / scan) on at most this many items each: the C5
+// generator has 1.6e9 directed draws, which is past what one call is trusted with.
+constexpr long long kChunk = 1ll << 28;
+
+// carry[c + 1] = carry[c] + the total of chunk c (its local exclusive scan's last
+// value + its last input), before the chunk is shifted
+__global__ void chunk_total_kernel(const int* __restrict__ out_last, const int* __restrict__ in_last,
+                                   int* __restrict__ carry, int c) {
+  carry[c + 1] = carry[c] + *out_last + *in_last;
+}
+
+__global__ void add_carry_kernel(long long len, int* __restrict__ out,
+                                 const int* __restrict__ carry) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < len) out[t] += *carry;
+}
+
 template <class T>
 void exclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
+  if (count <= kChunk) {
+    size_t tmp = 0;
+    GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)count, st));
+    DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
+    GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, in, out, (int)count, st));
+    return;
+  }
+  // chunks of kChunk, each shifted by the running total of the ones before
+  static_assert(sizeof(T) == sizeof(int), "chunked scan of int counts");
+  const int nc = (int)((count + kChunk - 1) / kChunk);
+  DevBuf<int> carry(nc + 1);
+  GE_HIP(hipMemsetAsync(carry.p, 0, sizeof(int) * (nc + 1), st));
   size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)count, st));
+  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)kChunk, st));
   DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, in, out, (int)count, st));
+  for (int c = 0; c < nc; ++c) {
+    const long long c0 = c * kChunk, len = std::min(kChunk, count - c0);
+    size_t t2 = tmp;
+    GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, t2, in + c0, out + c0, (int)len, st));
+    hipLaunchKernelGGL(chunk_total_kernel, dim3(1), dim3(1), 0, st,
+                       (const int*)(out + c0 + len - 1), (const int*)(in + c0 + len - 1), carry.p, c);
+    hipLaunchKernelGGL(add_carry_kernel, dim3(grid_for(len)), dim3(256), 0, st, len,
+                       (int*)(out + c0), carry.p + c);
+  }
+}
+
+// Valid keys per row (duplicates included), to cut the keys into row ranges of at
+// most kChunk for the sort.
+__global__ void key_rows_kernel(long long L, long long n, const u64* __restrict__ k,
+                                int* __restrict__ rowcnt) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < L && k[t] != kNoKey) atomicAdd(&rowcnt[(int)(k[t] / (u64)n)], 1);
+}
+
+// scatter each valid key into its row range's segment (order inside a segment is
+// free: the segment is sorted next)
+__global__ void scatter_keys_kernel(long long L, long long n, int nb, const int* __restrict__ bound,
+                                    const long long* __restrict__ boff, int* __restrict__ fill,
+                                    const u64* __restrict__ k, u64* __restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L || k[t] == kNoKey) return;
+  const int r = (int)(k[t] / (u64)n);
+  int b = 0;
+  while (b + 1 < nb && bound[b + 1] <= r) ++b;
+  out[boff[b] + atomicAdd(&fill[b], 1)] = k[t];
 }
 
 template <class T>
@@ -187,19 +245,65 @@ void rmat_device(ge_ctx* ctx, int n, long long draws, u64 seed, DCsr& out) {
   hipStream_t st = ctx->stream;
   int scale = 1;
   while ((1ll << scale) < n) ++scale;
-  const long long L = 2 * draws;
+  long long L = 2 * draws;
   GE_REQUIRE(L < (1ll << 31), "device R-MAT: more than 2^31 directed entries per call");
   DevBuf<u64> k(std::max(L, 1ll)), k2(std::max(L, 1ll));
   if (draws > 0)
     hipLaunchKernelGGL(rmat_keys_kernel, dim3(grid_for(draws)), dim3(256), 0, st, draws, scale,
                        (long long)n, splitmix64_host(seed), k.p);
   GE_HIP(hipGetLastError());
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, k.p, k2.p, (int)L, 0, 64, st));
-  {
+  if (L <= kChunk) {
+    size_t tmp = 0;
+    GE_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, k.p, k2.p, (int)L, 0, 64, st));
     DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
     // all 64 bits: the kNoKey sentinel sorts last
     GE_HIP(hipcub::DeviceRadixSort::SortKeys(scratch.p, tmp, k.p, k2.p, (int)L, 0, 64, st));
+  } else {
+    // Large inputs: cut the valid keys into row ranges of at most kChunk keys
+    // (row = key / n, so ranges of rows are ranges of keys), scatter each into its
+    // segment and sort the segments one by one -- the concatenation is sorted; the
+    // invalid keys are dropped here instead of sorting last.
+    DevBuf<int> rc(n);
+    GE_HIP(hipMemsetAsync(rc.p, 0, sizeof(int) * n, st));
+    hipLaunchKernelGGL(key_rows_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, (long long)n, k.p,
+                       rc.p);
+    std::vector<int> h_rc(n);
+    rc.download(h_rc.data(), n, st);
+    GE_HIP(hipStreamSynchronize(st));
+    std::vector<int> bound{0};
+    std::vector<long long> boff{0};
+    long long acc = 0, tot = 0;
+    for (int r = 0; r < n; ++r) {
+      GE_REQUIRE(h_rc[r] <= kChunk, "device R-MAT: one row exceeds a sort chunk");
+      if (acc + h_rc[r] > kChunk) {
+        bound.push_back(r);
+        boff.push_back(tot);
+        acc = 0;
+      }
+      acc += h_rc[r];
+      tot += h_rc[r];
+    }
+    const int nb = (int)bound.size();
+    DevBuf<int> d_bound(nb), d_fill(nb);
+    DevBuf<long long> d_boff(nb);
+    d_bound.upload(bound.data(), nb, st);
+    d_boff.upload(boff.data(), nb, st);
+    GE_HIP(hipMemsetAsync(d_fill.p, 0, sizeof(int) * nb, st));
+    hipLaunchKernelGGL(scatter_keys_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, (long long)n,
+                       nb, d_bound.p, d_boff.p, d_fill.p, k.p, k2.p);
+    GE_HIP(hipGetLastError());
+    size_t tmp = 0;
+    GE_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, k2.p, k.p, (int)kChunk, 0, 64, st));
+    DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
+    for (int b = 0; b < nb; ++b) {
+      const long long b0 = boff[b], b1 = b + 1 < nb ? boff[b + 1] : tot;
+      size_t t2 = tmp;
+      if (b1 > b0)
+        GE_HIP(hipcub::DeviceRadixSort::SortKeys(scratch.p, t2, k2.p + b0, k.p + b0, (int)(b1 - b0),
+                                                 0, 64, st));
+    }
+    std::swap(k.p, k2.p);  // the sorted keys are in k2 from here on, as in the small path
+    L = tot;
   }
   DevBuf<int> f(std::max(L, 1ll)), pos(std::max(L, 1ll));
   hipLaunchKernelGGL(unique_flags_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, k2.p, f.p);
