@@ -91,9 +91,13 @@ __global__ void emit_csr_kernel(long long L, long long n, const u64* __restrict_
   atomicAdd(&rowcnt[(int)(key / (u64)n)], 1);
 }
 
+// One block per row, grid-stride over rows: a dispatch covers at most 2^32 work
+// items, so a block per row of a 1e8-row matrix would silently drop rows.
+constexpr int kRowBlocks = 1 << 20;
+
 __global__ void row_of_entry_kernel(int n, const int* __restrict__ ip, int* __restrict__ row) {
-  const int i = blockIdx.x;
-  for (int e = ip[i] + threadIdx.x; e < ip[i + 1]; e += blockDim.x) row[e] = i;
+  for (int i = blockIdx.x; i < n; i += gridDim.x)
+    for (int e = ip[i] + threadIdx.x; e < ip[i + 1]; e += blockDim.x) row[e] = i;
 }
 
 __global__ void iota_kernel(int n, int* __restrict__ v) {
@@ -150,12 +154,13 @@ __global__ void lcc_copy_kernel(int n, const int* __restrict__ ip, const int* __
                                 const double* __restrict__ dx, const int* __restrict__ keep,
                                 const int* __restrict__ newid, const int* __restrict__ nip,
                                 int* __restrict__ nix, double* __restrict__ ndx) {
-  const int v = blockIdx.x;
-  if (!keep[v]) return;
-  const int o = nip[newid[v]] - ip[v];
-  for (int e = ip[v] + threadIdx.x; e < ip[v + 1]; e += blockDim.x) {
-    nix[o + e] = newid[ix[e]];  // a component is closed: every neighbour is kept
-    ndx[o + e] = dx[e];
+  for (int v = blockIdx.x; v < n; v += gridDim.x) {  // grid-stride (row_of_entry_kernel)
+    if (!keep[v]) continue;
+    const int o = nip[newid[v]] - ip[v];
+    for (int e = ip[v] + threadIdx.x; e < ip[v + 1]; e += blockDim.x) {
+      nix[o + e] = newid[ix[e]];  // a component is closed: every neighbour is kept
+      ndx[o + e] = dx[e];
+    }
   }
 }
 
@@ -333,7 +338,8 @@ void lcc_device(ge_ctx* ctx, const DCsr& A, DCsr& out) {
   if (n == 0) return;
   DevBuf<int> lab(n), row(std::max(A.nnz, 1ll)), changed(1);
   hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, lab.p);
-  hipLaunchKernelGGL(row_of_entry_kernel, dim3(n), dim3(64), 0, st, n, A.ip.p, row.p);
+  hipLaunchKernelGGL(row_of_entry_kernel, dim3(std::min(n, kRowBlocks)), dim3(64), 0, st, n,
+                     A.ip.p, row.p);
   for (int it = 0;; ++it) {
     GE_REQUIRE(it <= n + 1, "components: no convergence");
     GE_HIP(hipMemsetAsync(changed.p, 0, sizeof(int), st));
@@ -362,7 +368,8 @@ void lcc_device(ge_ctx* ctx, const DCsr& A, DCsr& out) {
   out.nnz = read_back(out.ip.p + k, st);
   out.ix.alloc(std::max(out.nnz, 1ll));
   out.dx.alloc(std::max(out.nnz, 1ll));
-  hipLaunchKernelGGL(lcc_copy_kernel, dim3(n), dim3(64), 0, st, n, A.ip.p, A.ix.p, A.dx.p,
+  hipLaunchKernelGGL(lcc_copy_kernel, dim3(std::min(n, kRowBlocks)), dim3(64), 0, st, n, A.ip.p,
+                     A.ix.p, A.dx.p,
                      keep.p, newid.p, out.ip.p, out.ix.p, out.dx.p);
   GE_HIP(hipGetLastError());
 }
