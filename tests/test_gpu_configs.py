@@ -82,7 +82,7 @@ def test_c3_level0_sampled_aggregates(ctx, oracle):
     assert np.isfinite(got).all()
 
 
-def test_c4_level0_sampled_aggregates(ctx, oracle):
+def test_c4_level0_sampled_aggregates(ctx, oracle, heartbeat):
     """configs[3] (C4, the headline): the 10M-id R-MAT LCC (n = 4.39M), device
     partition, level-0 forceAtlasMultilevel (2 iterations: the symmetric streamed
     kernel with its sweep hand-overs at full size) against the oracle on the largest
@@ -106,7 +106,8 @@ def test_c4_level0_sampled_aggregates(ctx, oracle):
     split = [a for a in order if 200 <= sizes[a] <= 2000][-4:]
     small = np.random.default_rng(4).choice(np.nonzero(sizes <= 200)[0], 100, replace=False)
     aggs = np.array(sorted(set(big) | set(split) | set(small.tolist())), dtype=np.int32)
-    want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
+    with heartbeat("C4 oracle aggregates"):
+        want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
     _progress(t0, "C4 oracle aggregates done")
     rows = np.concatenate([PT[1][PT[0][a]:PT[0][a + 1]] for a in aggs])
     assert sizes[aggs].max() > 40000
@@ -128,7 +129,7 @@ def _coarse_rows_numpy(L, PT, vA, rows):
     return out
 
 
-def test_c5_level0_sampled_aggregates(ctx, oracle):
+def test_c5_level0_sampled_aggregates(ctx, oracle, heartbeat):
     """configs[4] (C5) as an embed level: the 100M-id / 800M-draw R-MAT's LCC built
     on the device (examples/embedder.cpp:35-93), partition(A, 0.125) on the device
     (src/partitioner.cpp:1550-1893), P^T A P of level 0 on the device, and the
@@ -138,15 +139,12 @@ def test_c5_level0_sampled_aggregates(ctx, oracle):
     coarse rows of the sampled aggregates are checked against their definition."""
     import os
     import time
-    os.environ["GE_PROGRESS"] = "1"  # the device partition reports every ~10 s
     t0 = time.perf_counter()
     L = ctx.rmat_csr(100_000_000, 800_000_000, seed=12345, lcc=True)
     n, nnz = len(L[0]) - 1, len(L[1])
     _progress(t0, f"C5 LCC n={n} nnz={nnz} (device)")
-    try:
+    with heartbeat("C5 device partition"):
         hier = ctx.partition(L, 0.125)
-    finally:
-        del os.environ["GE_PROGRESS"]
     _progress(t0, f"C5 device partition levels {[h[2] for h in hier]}")
     PT = hier[0]
     m = PT[2]
@@ -168,9 +166,11 @@ def test_c5_level0_sampled_aggregates(ctx, oracle):
     del C
     cA = ge.uniform_stream(7, m * 3).reshape(m, 3)
     rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
-    got = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=2, seed=5)
+    with heartbeat("C5 level 0"):
+        got = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=2, seed=5)
     _progress(t0, f"C5 device level done (largest aggregate {sizes.max()})")
-    want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
+    with heartbeat("C5 oracle aggregates"):
+        want = oracle.force_atlas_ml_aggs(L, PT, vA, cA, rA, 3, aggs, iterations=2, seed=5)
     _progress(t0, "C5 oracle aggregates done")
     rows = np.concatenate([PT[1][PT[0][a]:PT[0][a + 1]] for a in aggs])
     assert sizes[aggs].max() == sizes.max()
@@ -178,10 +178,11 @@ def test_c5_level0_sampled_aggregates(ctx, oracle):
     assert np.isfinite(got).all()
 
 
-def test_c5_attraction_pass_sampled_rows(oracle):
+def test_c5_attraction_pass_sampled_rows(oracle, heartbeat):
     import time
     t0 = time.perf_counter()
-    A = ge.rmat_csr(100_000_000, 800_000_000, seed=12345)
+    with heartbeat("C5 host R-MAT"):
+        A = ge.rmat_csr(100_000_000, 800_000_000, seed=12345)
     _progress(t0, "C5 graph generated")
     n, nnz = len(A[0]) - 1, int(A[0][-1])
     dev = torch.device("cuda:0")
