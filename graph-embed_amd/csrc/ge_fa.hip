@@ -314,7 +314,17 @@ __global__ void fa_reduce_parts(int rows, int jblocks, const double* __restrict_
 // ---------------------------------------------------------------------------
 // Attraction + gravity + swing + update per row (serial CSR order).
 
-template <int D>
+// Coherent (agent-scope) accesses of the persistent coarsest-level kernel: its
+// coordinates cross XCDs between iterations, and the per-XCD L2s are not kept
+// coherent for plain loads and stores.
+__device__ __forceinline__ double coh_ld(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void coh_st(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int D, bool COH = false>
 __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D], double (&acc)[D],
                                            const double (&fprev)[D], double dip1, const FaConst& c,
                                            double* __restrict__ Fprev,
@@ -345,7 +355,8 @@ __device__ __forceinline__ void finish_row(int i, int li, const double (&xi)[D],
   if (!write) return;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    Xnext[(size_t)i * D + k] = F[k] * speed + xi[k];
+    if (COH) coh_st(&Xnext[(size_t)i * D + k], F[k] * speed + xi[k]);
+    else Xnext[(size_t)i * D + k] = F[k] * speed + xi[k];
     Fprev[(size_t)li * D + k] = F[k];
   }
 }
@@ -789,7 +800,7 @@ void launch_small(hipStream_t s, int n, int nnz, const int* ip, const int* ix, c
 // the T threads of the block: SU records per thread per round with all their
 // loads issued before the stores (a plain strided loop waits for one record at
 // a time).  Returns whether every staged value lies in the exact-division domain.
-template <int D, int T, int SU>
+template <int D, int T, int SU, bool COH = false>
 __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
                                               const double* __restrict__ dp1, int first, int cnt,
                                               double* rec) {
@@ -801,7 +812,8 @@ __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
     for (int u = 0; u < SU; ++u) {
       const int q = min(q0 + (int)threadIdx.x + T * u, cnt - 1);  // clamped into the range
 #pragma unroll
-      for (int k = 0; k < D; ++k) v[u][k] = X[(size_t)(first + q) * D + k];
+      for (int k = 0; k < D; ++k)
+        v[u][k] = COH ? coh_ld(&X[(size_t)(first + q) * D + k]) : X[(size_t)(first + q) * D + k];
       v[u][D] = dp1[first + q];
     }
 #pragma unroll
@@ -890,22 +902,24 @@ fa_repulse_grouped(int n, int rb, int re, const double* __restrict__ X,
 // LDS records) continuing the same ordered sum, then gravity, swing and the
 // update (:146-269).  Rows [rb, re); Fprev indexed by row - rb.  LINEAR: the
 // caller guarantees linlog == 0 and delta == 1 (the in-domain bodies use it).
-template <int D, int G, bool REPEL_ONE, bool LINEAR>
-__global__ void __launch_bounds__(kGrpT)
-fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
-                const double* __restrict__ dx, const double* __restrict__ X,
-                const double* __restrict__ dp1, FaConst c, double* __restrict__ Fprev,
-                double* __restrict__ Xnext) {
+template <int D, int G, bool REPEL_ONE, bool LINEAR, bool COH>
+__device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re,
+                                                  const int* __restrict__ ip,
+                                                  const int* __restrict__ ix,
+                                                  const double* __restrict__ dx,
+                                                  const double* __restrict__ X,
+                                                  const double* __restrict__ dp1, const FaConst& c,
+                                                  double* __restrict__ Fprev,
+                                                  double* __restrict__ Xnext, double* smem) {
   constexpr int W = Rec<D>::W;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
   double* rec = smem;
   double* tb = smem + (size_t)n * W;
   const int tid = threadIdx.x;
   const int g = tid % G;
-  const int i = rb + blockIdx.x * (kGrpT / G) + tid / G;
+  const int i = rb + blk * (kGrpT / G) + tid / G;
   const bool active = i < re;
   const bool ok =
-      stage_records<D, kGrpT, 4>(X, dp1, 0, n, rec) && (REPEL_ONE || weight_ok(c.repel));
+      stage_records<D, kGrpT, 4, COH>(X, dp1, 0, n, rec) && (REPEL_ONE || weight_ok(c.repel));
   double xi[D], acc[D], fprev[D];
   const int e0 = active ? ip[i] : 0;
   const int e1 = active ? ip[i + 1] : 0;
@@ -975,7 +989,100 @@ fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __
     }
   }
   if (active && g == 0)
-    finish_row<D>(i, i - rb, xi, acc, fprev, di, c, Fprev, Xnext, true);
+    finish_row<D, COH>(i, i - rb, xi, acc, fprev, di, c, Fprev, Xnext, true);
+}
+
+
+template <int D, int G, bool REPEL_ONE, bool LINEAR>
+__global__ void __launch_bounds__(kGrpT)
+fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
+                const double* __restrict__ dx, const double* __restrict__ X,
+                const double* __restrict__ dp1, FaConst c, double* __restrict__ Fprev,
+                double* __restrict__ Xnext) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  grouped_iteration<D, G, REPEL_ONE, LINEAR, false>(blockIdx.x, n, rb, re, ip, ix, dx, X, dp1, c,
+                                                    Fprev, Xnext, smem);
+}
+
+// ---------------------------------------------------------------------------
+// The coarsest level's 1e5 iterations (src/embed.cpp:586) as ONE launch: the
+// blocks of fa_grouped_step stay resident and run every iteration, separated by
+// a grid-wide barrier (the next iteration stages every block's coordinates).
+// The coordinates alternate between two buffers (iteration it reads buffer
+// it & 1), so one barrier per iteration suffices; each row's previous force
+// is read and written by the row's own leader lane only.  Coordinates are stored and staged with
+// agent-scope accesses; a block's stores have completed (s_waitcnt 0) before it
+// arrives, and the waiters poll the grid counter, so what a block stages after
+// the barrier is what every other block stored before it.
+//
+// bar layout (ints): [1] error flag, then a 128-byte line for the grid counter
+// and one per arrival group (kBarGroup blocks).
+// Counters only grow (target = arrivals * (iteration + 1)), so nothing is reset
+// between barriers.
+// A wait longer than ~limit ticks of the 100 MHz wall clock sets the error flag
+// and ends the kernel (every block then ends at its own next wait), so a
+// non-resident grid cannot hang the device.
+constexpr int kBarGroup = 16;
+constexpr int kBarLine = 32;  // ints per 128-byte line
+inline size_t persist_bar_ints(int nb) {
+  return (size_t)kBarLine * (2 + (nb + kBarGroup - 1) / kBarGroup);
+}
+
+__device__ __forceinline__ int coh_ldi(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 of each block: arrive at barrier number it (0-based) and wait for all.
+// Two levels: the last arrival of each group of kBarGroup blocks adds one to the
+// grid counter, which the waiters poll (one counter for every block was measured
+// slower: n = 998 22.3 against 19.7 us per iteration).
+__device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
+  int* cnt = bar + kBarLine;  // its own line, away from the error flag
+  const int ngroups = (nb + kBarGroup - 1) / kBarGroup;
+  const int grp = blockIdx.x / kBarGroup;
+  const int members = min(kBarGroup, nb - grp * kBarGroup);
+  int* gc = bar + kBarLine * (2 + grp);
+  const int old = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == members * (it + 1) - 1)  // the group's last arrival
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int target = ngroups * (it + 1);
+  const long long t0 = wall_clock64();
+  while (coh_ldi(cnt) < target) {
+    if (coh_ldi(bar + 1) != 0 || wall_clock64() - t0 > limit) {
+      __hip_atomic_store(bar + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+template <int D, int G, bool REPEL_ONE, bool LINEAR>
+__global__ void __launch_bounds__(kGrpT)
+fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__ ix,
+                      const double* __restrict__ dx, double* __restrict__ Xa,
+                      double* __restrict__ Xb, const double* __restrict__ dp1, FaConst c,
+                      double* __restrict__ Fprev, int* __restrict__ bar, int iterations,
+                      long long limit) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_ok;
+  for (int it = 0; it < iterations; ++it) {
+    const double* X = (it & 1) ? Xb : Xa;
+    double* Xn = (it & 1) ? Xa : Xb;
+    grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
+                                                     Fprev, Xn, smem);
+    if (it + 1 == iterations) break;
+    // this thread's coordinate stores have completed before the block arrives;
+    // the signal fences keep the compiler from moving memory accesses across
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __syncthreads();
+    if (threadIdx.x == 0) s_ok = grid_arrive_wait(bar, gridDim.x, it, limit) ? 1 : 0;
+    __syncthreads();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (!s_ok) return;
+  }
 }
 
 // Mid-size levels (grouped_cap < n <= kStreamMax): the same fused iteration
@@ -1432,6 +1539,81 @@ static void plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, d
   if (ev) GE_HIP(hipEventRecord(ev[2], s));
 }
 
+// All iterations of a small level (n <= grouped_cap, every row) in one launch of
+// fa_grouped_persistent.  The grid must fit the device at half its block
+// occupancy (so a co-running kernel cannot keep part of it from becoming
+// resident): the lanes per row halve from grouped_lanes(n) until it does.
+// Returns false (nothing launched) when no G fits; GE_PERSIST_REQUIRE=1 (tests)
+// makes that an error.  The result is in Xa for an even iteration count, in Xb
+// for an odd one.
+constexpr int kPersistMin = 128;  // fewer iterations: per-iteration launches
+template <int D>
+bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
+  const int n = pl->n;
+  if (n > grouped_cap(D) || pl->rb != 0 || pl->re != n) return false;
+  hipStream_t s = pl->ctx->stream;
+  const size_t lds = grouped_lds_bytes(n, D);
+  bool launched = false, fits = false;
+  DevBuf<int> bar;
+  auto go = [&](auto GG) {
+    constexpr int GC = decltype(GG)::value;
+    const int nb = (n + kGrpT / GC - 1) / (kGrpT / GC);
+    auto one = [&](auto RO, auto LI) {
+      constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
+      const void* fn = reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>);
+      if (lds > 65536)
+        GE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      int occ = 0;
+      GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kGrpT, lds));
+      if ((long long)nb * 2 > (long long)occ * pl->cus) return;
+      fits = true;
+      int dev = 0, khz = 0;
+      GE_HIP(hipGetDevice(&dev));
+      GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+      const long long limit = (long long)std::max(khz, 1000) * 2000;  // ~2 s per barrier
+      bar.alloc(persist_bar_ints(nb));
+      GE_HIP(hipMemsetAsync(bar.p, 0, sizeof(int) * bar.n, s));
+      hipLaunchKernelGGL((fa_grouped_persistent<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s,
+                         n, pl->ip, pl->ix, pl->dx, Xa, Xb, pl->dp1.p, pl->c, pl->fprev.p, bar.p,
+                         iterations, limit);
+      GE_HIP(hipGetLastError());
+      launched = true;
+    };
+    const bool lin = !pl->c.linlog && pl->c.delta == 1.0;
+    using T = std::true_type;
+    using F = std::false_type;
+    if (pl->c.repel == 1.0) {
+      if (lin) one(T(), T());
+      else one(T(), F());
+    } else {
+      if (lin) one(F(), T());
+      else one(F(), F());
+    }
+  };
+  for (int G = grouped_lanes(n); G >= 1 && !fits; G /= 2) {
+    switch (G) {
+      case 64: go(std::integral_constant<int, 64>()); break;
+      case 32: go(std::integral_constant<int, 32>()); break;
+      case 16: go(std::integral_constant<int, 16>()); break;
+      case 8: go(std::integral_constant<int, 8>()); break;
+      case 4: go(std::integral_constant<int, 4>()); break;
+      case 2: go(std::integral_constant<int, 2>()); break;
+      default: go(std::integral_constant<int, 1>()); break;
+    }
+  }
+  if (!launched) {
+    if (const char* e = std::getenv("GE_PERSIST_REQUIRE"))
+      if (*e == '1') throw Error(GE_ERR_STATE, "forceAtlas: the persistent kernel does not fit");
+    return false;
+  }
+  int err = 0;
+  GE_HIP(hipMemcpyAsync(&err, bar.p + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+  GE_HIP(hipStreamSynchronize(s));
+  if (err)
+    throw Error(GE_ERR_STATE, "forceAtlas: the persistent small-level kernel's grid barrier timed out");
+  return true;
+}
+
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
                    const double* d_dx, int dim, double* d_x, int iterations,
                    const ge_fa_params& p) {
@@ -1473,6 +1655,18 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
   double* cur = d_x;
   double* nxt = other.p;
   int it = 0;
+  if (p.mode == GE_MODE_STRICT && iterations >= kPersistMin && !std::getenv("GE_NO_PERSIST")) {
+    bool done = false;
+    dispatch_dim(dim, [&](auto Dc) {
+      done = launch_persistent<decltype(Dc)::value>(&pl, d_x, other.p, iterations);
+    });
+    if (done) {
+      if (iterations & 1)
+        GE_HIP(hipMemcpyAsync(d_x, other.p, sizeof(double) * n * dim, hipMemcpyDeviceToDevice, s));
+      GE_HIP(hipStreamSynchronize(s));
+      return;
+    }
+  }
   // Long runs (the coarsest level's 1e5 iterations) replay a captured graph of
   // kGraphSteps iterations: host launch overhead would otherwise dominate the
   // microsecond-scale kernels of a small level.

@@ -1177,7 +1177,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   std::vector<int> stamp(n, 0), moved(n / 2 + 1);
   auto t_last_note = now();
   long long stat[NCNT] = {0};
+  int rstat[NCNT] = {0};  // this round's list sizes (GE_PROFILE_ROUNDS)
+  const bool prof_rounds = prof && std::getenv("GE_PROFILE_ROUNDS");
   do {
+    std::fill(rstat, rstat + NCNT, 0);
     ++rounds;
     const auto t0 = now();
     for (int pass = 0; pass < matching; ++pass) {
@@ -1202,6 +1205,9 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
         GE_HIP(hipStreamSynchronize(st));
         for (int c = C_SMALL; c <= C_CAND; ++c) stat[c] += h_cnt[c];
+        stat[C_HUGE] += h_cnt[C_HUGE];
+        for (int c : {(int)C_SMALL, (int)C_MID, (int)C_BIG, (int)C_HUGE, (int)C_PROP, (int)C_CAND})
+          rstat[c] += h_cnt[c];
       }
     }
     GE_HIP(hipGetLastError());
@@ -1211,7 +1217,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
     if (prof)
-      for (int c = C_DIRTY; c <= C_G; ++c) stat[c] += h_cnt[c];  // previous round's contraction
+      for (int c = C_DIRTY; c <= C_G; ++c) {
+        stat[c] += h_cnt[c];  // previous round's contraction
+        rstat[c] = h_cnt[c];
+      }
     rb.top = *h_top;
     if (h_cnt[C_OVF])
       throw Error(GE_ERR_STATE, h_cnt[C_OVF] == 2 ? "partition_device: resolve did not converge"
@@ -1319,8 +1328,14 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       std::fprintf(stderr, "partition_device: round %d, %d aggregates, %lld merges, %.0f s\n",
                    rounds, M, total_merges, secs(t_start, t_last_note));
     }
-    if (prof && std::getenv("GE_PROFILE_ROUNDS"))
-      std::fprintf(stderr, "round %d alive %d merges %d pool %llu\n", rounds, M, nm, rb.top);
+    if (prof_rounds)  // rescans by class (both passes), proposers, candidates; the
+                      // previous round's contraction: dirty lists by table class
+      std::fprintf(stderr,
+                   "round %d alive %d merges %d pool %llu small %d mid %d big %d huge %d prop %d "
+                   "cand %d dirty %d w %d b %d g %d\n",
+                   rounds, M, nm, rb.top, rstat[C_SMALL], rstat[C_MID], rstat[C_BIG],
+                   rstat[C_HUGE], rstat[C_PROP], rstat[C_CAND], rstat[C_DIRTY], rstat[C_W],
+                   rstat[C_B], rstat[C_G]);
   } while (1.0 * M / M_prev < stall);  // :1838
   GE_HIP(hipStreamSynchronize(st));
   snap();  // :1840-1852
@@ -1332,9 +1347,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                  t_compact);
   if (prof)
     std::fprintf(stderr,
-                 "partition_device lists (sums over passes): rescans small %lld mid %lld big %lld, "
-                 "proposers %lld, candidates %lld; dirty %lld (wave %lld block %lld global %lld)\n",
-                 stat[C_SMALL], stat[C_MID], stat[C_BIG], stat[C_PROP], stat[C_CAND], stat[C_DIRTY],
+                 "partition_device lists (sums over passes): rescans small %lld mid %lld big %lld "
+                 "huge %lld, proposers %lld, candidates %lld; dirty %lld (wave %lld block %lld "
+                 "global %lld)\n",
+                 stat[C_SMALL], stat[C_MID], stat[C_BIG], stat[C_HUGE], stat[C_PROP], stat[C_CAND],
+                 stat[C_DIRTY],
                  stat[C_W], stat[C_B], stat[C_G]);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;

@@ -225,6 +225,51 @@ def test_fa_small_level_graph_replay(ctx, oracle):
     assert np.array_equal(ctx.force_atlas(A, 3, iterations=3000, seed=77), want)
 
 
+@pytest.mark.parametrize("n,dim,grp,its", [(300, 3, "0", 200), (700, 2, "0", 131),
+                                            (1300, 4, "0", 128), (2900, 3, "32", 129),
+                                            (1068, 3, "16", 140), (500, 1, "64", 257)])
+def test_fa_persistent_small_level(ctx, oracle, monkeypatch, n, dim, grp, its):
+    """Small levels with >= 128 iterations run every iteration in one launch
+    (fa_grouped_persistent: resident blocks, grid barrier, coordinates in two
+    alternating buffers); odd and even counts, G lanes per row."""
+    monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
+    if grp != "0":
+        monkeypatch.setenv("GE_GRP_G", grp)
+    A = G.rmat(n, 6 * n, seed=n + dim)
+    X0 = G.random_coords(n, dim, seed=n)
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=its)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=its), want)
+
+
+def test_fa_persistent_params_and_domain(ctx, oracle, monkeypatch):
+    """Non-default parameters (repel != 1, weights off) and a start outside the
+    exact-division domain (the general bodies) in the persistent kernel."""
+    monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
+    A = G.largest_component(G.rmat(600, 3000, seed=8))
+    n = len(A[0]) - 1
+    X0 = G.random_coords(n, 3, seed=5)
+    kw = dict(ks=0.2, ksmax=2.0, repel=1.5, attract=0.7, gravity=2.0, use_weights=0)
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=150, **kw)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=150, **kw), want)
+    X0[7, 2] = 1e-70
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=130)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=130), want)
+
+
+def test_fa_persistent_matches_graph_replay_long(ctx, monkeypatch):
+    """C4's coarsest-level size (n ~ 1068, 64 lanes per row) over 20 000
+    iterations: the persistent launch equals the per-iteration graph replay (which
+    the oracle pins above) bit for bit."""
+    A = G.largest_component(G.rmat(1400, 9000, seed=31))
+    n = len(A[0]) - 1
+    assert 900 < n <= 3072
+    X0 = G.random_coords(n, 3, seed=12)
+    monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
+    got = ctx.force_atlas(A, 3, coords=X0, iterations=20000)
+    monkeypatch.setenv("GE_NO_PERSIST", "1")
+    assert np.array_equal(got, ctx.force_atlas(A, 3, coords=X0, iterations=20000))
+
+
 def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     # the coarsest level runs the default 100000 iterations (src/embed.cpp:586);
     # chaos amplifies any op-order difference far beyond 1e-5 over that horizon
