@@ -61,6 +61,14 @@ constexpr int kBigLen = 16384;     // scan: one 256-thread block up to this, the
 constexpr int kWaveNeed = 64;      // rebuild: one wave (128-slot LDS table) up to this
 constexpr int kBlockNeed = 2048;   // rebuild: one block (4096-slot LDS table) up to this
 constexpr int kBlockSlots = 4096;
+// Hub lists (longer than kPatchMin) are patched in place after a round instead of
+// rebuilt (patch_list): at most kPatchGone absorbed neighbours and a partner list
+// of at most kPatchGone entries, in LDS sets of kPatchSet slots.
+constexpr int kPatchMin = kBlockNeed;
+constexpr int kPatchGone = 1024;
+constexpr int kPatchSet = 4096;
+constexpr int kPairCap = 1 << 22;
+constexpr int kPatchU = 16;
 
 enum {
   C_SMALL,
@@ -78,6 +86,10 @@ enum {
   C_ALIVE2,
   C_CAND2,
   C_HUGE,
+  C_PAIR,   // (hub, absorbed neighbour) pairs of this round's contraction
+  C_PATCH,  // hub lists patched in place this round (profiling)
+  C_PTOP,   // bucket space handed out to the hubs' absorbed-neighbour lists
+  C_PF_SHORT, C_PF_SIZE, C_PF_FIT,  // lists rebuilt instead: short, sets too small, no room
   NCNT
 };
 
@@ -132,6 +144,11 @@ struct Dev {
   unsigned long long* gtop;
   unsigned long long* pool_top;
   long long pool_cap;
+  int2* pairs;  // (hub, absorbed neighbour), kPairCap
+  int* pcnt;    // per hub: pairs counted (mark_dirty), then the bucket fill cursor
+  int2* pinfo;  // per hub: (bucket offset, pair count)
+  int* pbuf;    // the buckets: each hub's absorbed neighbours, kPairCap
+  int patch;    // 0: every dirty list is rebuilt (GE_PARTITION_NO_PATCH)
 };
 
 __device__ inline int lane_id() { return threadIdx.x & 63; }
@@ -658,13 +675,25 @@ __global__ void mark_dirty_kernel(Dev d) {
     const long long o = d.aoff[gone];
     for (int b = 0; b < len; b += 64) {
       const int t = b + lane;
-      bool mk = false;
+      bool mk = false, pr = false;
       int k = 0;
       if (t < len) {
         k = d.akey[o + t];
-        mk = k != keep && d.rep[k] == k && atomicCAS(&d.dirty[k], 0, 1) == 0;
+        const bool live = k != keep && d.rep[k] == k;
+        mk = live && atomicCAS(&d.dirty[k], 0, 1) == 0;
+        pr = d.patch && live && d.alen[k] > kPatchMin;  // a hub: patched, not rebuilt
       }
       wave_append(d.dlist, &d.cnt[C_DIRTY], mk, k);
+      const unsigned long long pm = __ballot(pr);
+      if (pm) {  // the pair (k, gone), capped (over the cap: no hub is patched this round)
+        const int leader = __ffsll((long long)pm) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&d.cnt[C_PAIR], __popcll(pm));
+        base = __shfl(base, leader);
+        const int at = base + __popcll(pm & ((1ull << lane) - 1ull));
+        if (pr && at < kPairCap) d.pairs[at] = make_int2(k, gone);
+        if (pr) atomicAdd(&d.pcnt[k], 1);
+      }
     }
   }
 }
@@ -697,6 +726,9 @@ __global__ void classify_kernel(Dev d) {
       d.lg[at] = u;
       d.gofs[at] = (long long)atomicAdd(d.gtop, (unsigned long long)slots);
       d.gmask[at] = (int)slots - 1;
+      const int pc = d.pcnt[u];  // this hub's bucket of absorbed neighbours
+      d.pinfo[u] = make_int2(pc > 0 ? atomicAdd(&d.cnt[C_PTOP], pc) : 0, pc);
+      d.pcnt[u] = 0;
     }
   }
 }
@@ -788,6 +820,185 @@ __device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int 
   __syncthreads();
 }
 
+// the pairs into their hubs' buckets (when every pair was stored)
+__global__ void pair_scatter_kernel(Dev d) {
+  const int np = d.cnt[C_PAIR];
+  if (np > kPairCap) return;
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < np; x += gridDim.x * blockDim.x) {
+    const int2 pr = d.pairs[x];
+    const int at = d.pinfo[pr.x].x + atomicAdd(&d.pcnt[pr.x], 1);
+    if (at >= 0 && at < kPairCap) d.pbuf[at] = pr.y;  // (always: every pair's hub is in lg)
+  }
+}
+
+// ---- hub lists patched in place ----------------------------------------------
+// A hub's list changes in a round only where a neighbour was absorbed: that
+// entry goes and its weight moves to the keeper's entry (which may be new), and
+// when the hub itself kept a merge its partner's entries (renamed) are added and
+// the partner's own entry goes.  mark_dirty_kernel recorded (hub, absorbed) pairs;
+// the hub's list is read twice (coalesced, no gathers): once to find the absorbed
+// entries, once to find the entries of the keys that receive weight.  The result
+// is the rebuild's list up to entry order (lists keep no order; integer weights
+// sum exactly in any order).  Returns false, having written nothing, when a set
+// would overflow or the list outgrows its capacity: the caller rebuilds.
+struct PatchLds {
+  int gk[kPatchSet];    // absorbed neighbours in the list (set)
+  int ik[kPatchSet];    // keys that receive weight (set)
+  int ipos[kPatchSet];  // their position in the list, -1: a new entry
+  double iw[kPatchSet];
+  int del[kPatchGone + 1];  // positions of the absorbed entries
+  int ngone, ndel, nnew, fill, ok;
+};
+
+__device__ inline int set_insert(int* keys, int key) {
+  unsigned h = slot_hash(key) & (kPatchSet - 1);
+  while (true) {
+    const int prev = atomicCAS(&keys[h], -1, key);
+    if (prev == -1 || prev == key) return (int)h;
+    h = (h + 1) & (kPatchSet - 1);
+  }
+}
+
+__device__ inline int set_find(const int* keys, int key) {
+  unsigned h = slot_hash(key) & (kPatchSet - 1);
+  while (true) {
+    const int k = keys[h];
+    if (k == key) return (int)h;
+    if (k == -1) return -1;
+    h = (h + 1) & (kPatchSet - 1);
+  }
+}
+
+__device__ bool patch_list(const Dev& d, int u, PatchLds& s, int tid, int nt) {
+  const int npairs = d.cnt[C_PAIR];
+  const int g = d.partner[u];
+  const int len = d.alen[u];
+  const long long o = d.aoff[u];
+  if (!d.patch) return false;
+  if (len <= kPatchMin || npairs > kPairCap || (g >= 0 && d.alen[g] > kPatchGone)) {
+    if (tid == 0) atomicAdd(&d.cnt[len <= kPatchMin ? C_PF_SHORT : C_PF_SIZE], 1);
+    return false;  // uniform over the block
+  }
+  for (int x = tid; x < kPatchSet; x += nt) {
+    s.gk[x] = -1;
+    s.ik[x] = -1;
+    s.ipos[x] = -1;
+    s.iw[x] = 0.0;
+  }
+  if (tid == 0) {
+    s.ngone = g >= 0 ? 1 : 0;
+    s.ndel = s.nnew = s.fill = 0;
+  }
+  __syncthreads();
+  const int2 pi = d.pinfo[u];
+  if (pi.y + s.ngone > kPatchGone) {  // uniform
+    if (tid == 0) atomicAdd(&d.cnt[C_PF_SIZE], 1);
+    return false;
+  }
+  if (tid == 0 && g >= 0) set_insert(s.gk, g);  // the partner's own entry goes
+  for (int x = tid; x < pi.y; x += nt) set_insert(s.gk, d.pbuf[pi.x + x]);
+  __syncthreads();
+  if (tid == 0) s.ngone += pi.y;
+  // the keys that receive weight: the absorbed neighbours' keepers, and the
+  // partner's entries renamed (its edge to u goes into alpha, :1767-1770)
+  for (int x = tid; x < pi.y; x += nt) {
+    const int r = d.rep[d.pbuf[pi.x + x]];
+    if (r != u) set_insert(s.ik, r);
+  }
+  if (g >= 0) {
+    const int glen = d.alen[g];
+    const long long go = d.aoff[g];
+    for (int t = tid; t < glen; t += nt) {
+      const int r = d.rep[d.akey[go + t]];
+      if (r != u) atomicAdd(&s.iw[set_insert(s.ik, r)], d.aw[go + t]);
+    }
+  }
+  __syncthreads();
+  // one pass over the list (kPatchU coalesced loads in flight per thread): the
+  // absorbed entries go (their weight to their keeper's key), and the entries of
+  // the keys that receive weight are located
+  for (int t0 = 0; t0 < len; t0 += nt * kPatchU) {
+    int k[kPatchU];
+#pragma unroll
+    for (int q = 0; q < kPatchU; ++q) {
+      const int t = t0 + q * nt + tid;
+      k[q] = t < len ? d.akey[o + t] : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < kPatchU; ++q) {
+      if (k[q] < 0) continue;
+      const int t = t0 + q * nt + tid;
+      if (set_find(s.gk, k[q]) >= 0) {
+        s.del[atomicAdd(&s.ndel, 1)] = t;
+        const int r = d.rep[k[q]];
+        const int sl = r != u ? set_find(s.ik, r) : -1;  // (inserted above)
+        if (sl >= 0) atomicAdd(&s.iw[sl], d.aw[o + t]);
+      } else {
+        const int sl = set_find(s.ik, k[q]);
+        if (sl >= 0) s.ipos[sl] = t;
+      }
+    }
+  }
+  __syncthreads();
+  for (int x = tid; x < kPatchSet; x += nt)
+    if (s.ik[x] >= 0 && s.ipos[x] < 0) atomicAdd(&s.nnew, 1);
+  __syncthreads();
+  const int ndel = s.ndel, nnew = s.nnew;
+  const int newlen = len - ndel + nnew;
+  // every absorbed neighbour was found (the lists are symmetric), and the list fits
+  if (ndel != s.ngone || newlen > d.acap[u]) {
+    if (tid == 0) atomicAdd(&d.cnt[C_PF_FIT], 1);
+    return false;
+  }
+  for (int x = tid; x < kPatchSet; x += nt) {
+    const int k = s.ik[x];
+    if (k < 0) continue;
+    if (s.ipos[x] >= 0) {
+      d.aw[o + s.ipos[x]] = d.aw[o + s.ipos[x]] + s.iw[x];  // integers: exact
+    } else {
+      const int f = atomicAdd(&s.fill, 1);
+      const int at = f < ndel ? s.del[f] : len + (f - ndel);
+      d.akey[o + at] = k;
+      d.aw[o + at] = s.iw[x];
+    }
+  }
+  drain();
+  __syncthreads();
+  // close the remaining holes H = del[nnew, ndel) in parallel: the list ends at
+  // L = len - |H|; the holes below L take the live entries of [L, len) (the
+  // tail holds exactly as many live entries as there are holes below L)
+  const int nh = ndel > nnew ? ndel - nnew : 0;
+  if (nh > 0) {
+    const int* h = s.del + nnew;
+    const int L = len - nh;
+    int* tail = s.gk;                    // [nh] flags: tail slot is a hole
+    int* below = s.gk + kPatchGone + 1;  // holes below L
+    int* live = s.ipos;                  // live tail positions (ipos is no longer needed)
+    for (int x = tid; x < nh; x += nt) tail[x] = 0;
+    if (tid == 0) s.fill = 0;  // reused: count of holes below L
+    __syncthreads();
+    for (int x = tid; x < nh; x += nt) {
+      if (h[x] >= L) tail[h[x] - L] = 1;
+      else below[atomicAdd(&s.fill, 1)] = h[x];
+    }
+    if (tid == 0) s.nnew = 0;  // reused: count of live tail slots
+    __syncthreads();
+    for (int y = tid; y < nh; y += nt)
+      if (!tail[y]) live[atomicAdd(&s.nnew, 1)] = L + y;
+    __syncthreads();
+    for (int x = tid; x < s.fill; x += nt) {
+      d.akey[o + below[x]] = d.akey[o + live[x]];
+      d.aw[o + below[x]] = d.aw[o + live[x]];
+    }
+  }
+  if (tid == 0) {
+    d.alen[u] = newlen;
+    atomicAdd(&d.cnt[C_PATCH], 1);
+  }
+  __syncthreads();
+  return true;
+}
+
 __global__ void __launch_bounds__(64) rebuild_wave_kernel(Dev d) {
   __shared__ int tk[2 * kWaveNeed];
   __shared__ double tw[2 * kWaveNeed];
@@ -816,14 +1027,24 @@ __global__ void __launch_bounds__(256) rebuild_block_kernel(Dev d) {
 __global__ void __launch_bounds__(1024) rebuild_global_kernel(Dev d) {
   __shared__ int s_cnt;
   __shared__ long long s_dst;
+  __shared__ PatchLds s_patch;
   const int count = d.cnt[C_G];
-  for (int x = blockIdx.x; x < count; x += gridDim.x)
+  for (int x = blockIdx.x; x < count; x += gridDim.x) {
+    const bool patched = patch_list(d, d.lg[x], s_patch, threadIdx.x, (int)blockDim.x);
+    if (threadIdx.x == 0) d.pcnt[d.lg[x]] = 0;  // the bucket cursor, for the next round
+    if (patched) continue;
+    __syncthreads();
     rebuild_list(d, d.lg[x], d.gkey + d.gofs[x], d.gw + d.gofs[x], d.gmask[x], threadIdx.x,
                  (int)blockDim.x, &s_cnt, &s_dst);
+  }
 }
 
 __global__ void dirty_reset_kernel(Dev d, int round) {
   const int count = d.cnt[C_DIRTY];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // for the next contraction
+    d.cnt[C_PAIR] = 0;
+    d.cnt[C_PTOP] = 0;
+  }
   for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < count; x += gridDim.x * blockDim.x) {
     const int u = d.dlist[x];
     d.dirty[u] = 0;
@@ -1011,6 +1232,9 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DevBuf<double> gw(gcap);
   DevBuf<unsigned long long> tops(2);  // [0] pool top, [1] global-table top
   DevBuf<int2> d_changes(n / 2 + 1);
+  DevBuf<int2> pairs(kPairCap), pinfo(n);
+  DevBuf<int> pcnt(n), pbuf(kPairCap);
+  GE_HIP(hipMemsetAsync(pcnt.p, 0, sizeof(int) * n, st));
 
   Dev d{};
   d.N = n;
@@ -1057,6 +1281,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d.gtop = tops.p + 1;
   d.pool_top = tops.p;
   d.pool_cap = pool_cap;
+  d.pairs = pairs.p;
+  d.pcnt = pcnt.p;
+  d.pinfo = pinfo.p;
+  d.pbuf = pbuf.p;
+  d.patch = std::getenv("GE_PARTITION_NO_PATCH") == nullptr;
 
   note("buffers allocated");
   GE_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * NCNT, st));
@@ -1170,6 +1399,8 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   } pinned_top{h_top};
 
   int alist_len = n;
+  int mid_blocks = 1024;  // GE_PART_MID_BLOCKS: tuning
+  if (const char* e = std::getenv("GE_PART_MID_BLOCKS")) mid_blocks = std::max(1, std::atoi(e));
   double t_dev = 0, t_host = 0, t_compact = 0;
   long long total_merges = 0;
   int rounds = 0, compactions = 0;
@@ -1189,7 +1420,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
                          pass, alist_len, rounds, rounds == 1 ? 1 : 0);
       hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_mid_kernel, dim3(1024), dim3(256), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_mid_kernel, dim3(mid_blocks), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(scan_big_kernel<256>, dim3(1024), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(scan_big_kernel<1024>, dim3(256), dim3(1024), 0, st, d, pass);
       hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
@@ -1216,11 +1447,16 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     GE_HIP(hipStreamSynchronize(st));
     if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
-    if (prof)
+    if (prof) {
       for (int c = C_DIRTY; c <= C_G; ++c) {
         stat[c] += h_cnt[c];  // previous round's contraction
         rstat[c] = h_cnt[c];
       }
+      for (int c : {(int)C_PATCH, (int)C_PF_SHORT, (int)C_PF_SIZE, (int)C_PF_FIT}) {
+        rstat[c] = h_cnt[c] - (int)stat[c];  // these counters accumulate
+        stat[c] = h_cnt[c];
+      }
+    }
     rb.top = *h_top;
     if (h_cnt[C_OVF])
       throw Error(GE_ERR_STATE, h_cnt[C_OVF] == 2 ? "partition_device: resolve did not converge"
@@ -1265,6 +1501,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       hipLaunchKernelGGL(merge_apply_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, st, d, rounds);
       hipLaunchKernelGGL(mark_dirty_kernel, dim3(blocks_for(nm, 4)), dim3(256), 0, st, d);
       hipLaunchKernelGGL(classify_kernel, dim3(1024), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(pair_scatter_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(rebuild_wave_kernel, dim3(8192), dim3(64), 0, st, d);
       hipLaunchKernelGGL(rebuild_block_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(rebuild_global_kernel, dim3(256), dim3(1024), 0, st, d);
@@ -1332,10 +1569,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                       // previous round's contraction: dirty lists by table class
       std::fprintf(stderr,
                    "round %d alive %d merges %d pool %llu small %d mid %d big %d huge %d prop %d "
-                   "cand %d dirty %d w %d b %d g %d\n",
+                   "cand %d dirty %d w %d b %d g %d patched %d rebuilt short %d size %d fit %d\n",
                    rounds, M, nm, rb.top, rstat[C_SMALL], rstat[C_MID], rstat[C_BIG],
                    rstat[C_HUGE], rstat[C_PROP], rstat[C_CAND], rstat[C_DIRTY], rstat[C_W],
-                   rstat[C_B], rstat[C_G]);
+                   rstat[C_B], rstat[C_G], rstat[C_PATCH], rstat[C_PF_SHORT], rstat[C_PF_SIZE],
+                   rstat[C_PF_FIT]);
   } while (1.0 * M / M_prev < stall);  // :1838
   GE_HIP(hipStreamSynchronize(st));
   snap();  // :1840-1852
@@ -1349,10 +1587,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     std::fprintf(stderr,
                  "partition_device lists (sums over passes): rescans small %lld mid %lld big %lld "
                  "huge %lld, proposers %lld, candidates %lld; dirty %lld (wave %lld block %lld "
-                 "global %lld)\n",
+                 "global %lld, of which patched %lld; rebuilt: short %lld, sets %lld, room %lld)\n",
                  stat[C_SMALL], stat[C_MID], stat[C_BIG], stat[C_HUGE], stat[C_PROP], stat[C_CAND],
                  stat[C_DIRTY],
-                 stat[C_W], stat[C_B], stat[C_G]);
+                 stat[C_W], stat[C_B], stat[C_G], stat[C_PATCH], stat[C_PF_SHORT], stat[C_PF_SIZE],
+                 stat[C_PF_FIT]);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;
     std::cout << "level 0: " << n << " aggregates" << std::endl;
