@@ -148,6 +148,11 @@ struct Dev {
   int* pcnt;    // per hub: pairs counted (mark_dirty), then the bucket fill cursor
   int2* pinfo;  // per hub: (bucket offset, pair count)
   int* pbuf;    // the buckets: each hub's absorbed neighbours, kPairCap
+  // what the last pass-0 scan of a vertex found besides its argmax: the argmax,
+  // its entry's weight and the best eta of every other entry (see classify_scan)
+  int* t2arg;
+  double* t2w;
+  double* t2b2;
   int patch;    // 0: every dirty list is rebuilt (GE_PARTITION_NO_PATCH)
 };
 
@@ -217,11 +222,43 @@ __device__ inline double eta_of(const Dev& d, double w, double au, int k) {
   return 2.0 * (w / d.T - au * d.alpha[k]);  // :1715 (no contraction: -ffp-contract=off)
 }
 
-__device__ inline void scan_store(const Dev& d, int u, double be, int bk, bool& prop) {
+__device__ inline void scan_store(const Dev& d, int u, int pass, double be, int bk, double bw,
+                                  double be2, bool& prop) {
   d.best[u] = be;
   d.arg[u] = bk == INT_MAX ? -1 : bk;
   prop = bk != INT_MAX && (!d.positive || be > 0.0);
+  if (pass == 0) {
+    d.t2arg[u] = bk == INT_MAX ? -1 : bk;
+    d.t2w[u] = bw;
+    d.t2b2[u] = be2;
+  }
 }
+
+// Running (argmax, its weight, best eta of the other entries) of a scan.
+struct Top2 {
+  double be = -INFINITY, bw = 0.0, be2 = -INFINITY;
+  int bk = INT_MAX;
+  __device__ void add(double e, int k, double w) {
+    if (better(e, k, be, bk)) {
+      be2 = fmax(be2, be);
+      be = e;
+      bk = k;
+      bw = w;
+    } else {
+      be2 = fmax(be2, e);
+    }
+  }
+  __device__ void merge(double e, int k, double w, double e2) {  // another scan's state
+    if (better(e, k, be, bk)) {
+      be2 = fmax(fmax(be2, be), e2);
+      be = e;
+      bk = k;
+      bw = w;
+    } else {
+      be2 = fmax(be2, fmax(e, e2));
+    }
+  }
+};
 
 // ---- scan (:1703-1726) -----------------------------------------------------
 // Which alive vertices the reference's scan would give a different answer than
@@ -239,7 +276,7 @@ __device__ inline void scan_store(const Dev& d, int u, double be, int bk, bool& 
 //    with max_eta = -inf, the reference's own rule).
 // Vertices that keep their result and have a usable candidate go straight to the
 // proposer list; the rescans are split by list length.
-__global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full) {
+__global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full, int last) {
   __shared__ int s_app[6];
   const int stride = gridDim.x * blockDim.x;
   const int rounds = (L + stride - 1) / stride;
@@ -254,15 +291,47 @@ __global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full
         const bool tu = d.touched[u];
         const int a = d.arg[u];
         if (pass == 0) {
-          resc = full || !d.incremental || d.chg[u] == round - 1 || d.late[u] ||
-                 (a >= 0 && d.kst[a] == round - 1);
+          resc = full || !d.incremental || d.chg[u] == round - 1;
+          if (!resc && (d.late[u] || (a >= 0 && d.kst[a] == round - 1))) {
+            // The last pass-0 scan's argmax a0 may have lost eta (its alpha grew)
+            // or been excluded since (late).  u's list and alpha are unchanged
+            // since that scan (chg), and every other alpha only grew, so every
+            // other entry's eta is still <= the be2 that scan recorded: if a0's
+            // eta now, computed as a scan computes it, exceeds be2, a0 is the
+            // argmax and that eta the max -- what a rescan returns.
+            const int a0 = d.t2arg[u];
+            bool skip = false;
+            if (a0 >= 0) {
+              const double e = eta_of(d, d.t2w[u], d.alpha[u], a0);
+              if (e > d.t2b2[u]) {
+                d.best[u] = e;
+                d.arg[u] = a0;
+                d.late[u] = 0;
+                skip = true;
+              }
+            }
+            resc = !skip;
+          }
         } else if (!tu) {
           resc = !d.incremental || (a >= 0 && d.touched[a]);
+          if (resc && d.incremental && last && d.positive && a >= 0 && a == d.t2arg[u] &&
+              d.t2b2[u] <= 0.0) {
+            // The last pass under positiveMerging: every entry but a has eta <=
+            // be2 <= 0 (the pass-0 bound above), so u's best over its untouched
+            // entries is <= 0.  u cannot propose, and a proposer i pointing at u
+            // (best[i] > 0) passes !(best[i] < best[u]) for any best[u] <= 0: the
+            // bound stands in for the rescan.  Nothing reads it after this pass
+            // (late: the next pass 0 goes through the bound or rescans).
+            d.best[u] = d.t2b2[u];
+            d.arg[u] = -1;
+            d.late[u] = 1;
+            resc = false;
+          }
         } else {
           resc = d.best[u] == -INFINITY;
         }
         if (resc) len = d.alen[u];
-        else keepprop = !tu && a >= 0 && (!d.positive || d.best[u] > 0.0);
+        else keepprop = !tu && d.arg[u] >= 0 && (!d.positive || d.best[u] > 0.0);
       }
     }
     int* const lists[3] = {d.small, d.mid, d.prop};
@@ -285,20 +354,16 @@ __global__ void scan_small_kernel(Dev d, int pass) {
     if (x < count) {
       u = d.small[x];
       const int len = d.alen[u];
-      double be = -INFINITY;
-      int bk = INT_MAX;
+      Top2 b;
       const double au = d.alpha[u];
       const long long o = d.aoff[u];
       for (int t = 0; t < len; ++t) {
         const int k = d.akey[o + t];
         if (pass > 0 && d.touched[k]) continue;
-        const double e = eta_of(d, d.aw[o + t], au, k);
-        if (better(e, k, be, bk)) {
-          be = e;
-          bk = k;
-        }
+        const double w = d.aw[o + t];
+        b.add(eta_of(d, w, au, k), k, w);
       }
-      scan_store(d, u, be, bk, prop);
+      scan_store(d, u, pass, b.be, b.bk, b.bw, b.be2, prop);
       d.late[u] = pass > 0;
       prop = prop && !d.touched[u];
     }
@@ -311,7 +376,7 @@ __global__ void scan_small_kernel(Dev d, int pass) {
 
 // Scan entries [b, e) of u's list with `stride` cooperating threads, 4 in flight.
 __device__ inline void scan_range(const Dev& d, int pass, int u, int b, int e, int stride,
-                                  double& be, int& bk) {
+                                  Top2& bt) {
   const double au = d.alpha[u];
   const long long o = d.aoff[u];
   int t = b;
@@ -332,33 +397,23 @@ __device__ inline void scan_range(const Dev& d, int pass, int u, int b, int e, i
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (tc[q]) continue;
-      const double eta = 2.0 * (w[q] / d.T - au * a[q]);
-      if (better(eta, k[q], be, bk)) {
-        be = eta;
-        bk = k[q];
-      }
+      bt.add(2.0 * (w[q] / d.T - au * a[q]), k[q], w[q]);  // eta_of
     }
   }
   for (; t < e; t += stride) {
     const int k = d.akey[o + t];
     if (pass > 0 && d.touched[k]) continue;
-    const double eta = eta_of(d, d.aw[o + t], au, k);
-    if (better(eta, k, be, bk)) {
-      be = eta;
-      bk = k;
-    }
+    const double w = d.aw[o + t];
+    bt.add(eta_of(d, w, au, k), k, w);
   }
 }
 
-__device__ inline void wave_argmax(double& be, int& bk) {
+__device__ inline void wave_argmax(Top2& b) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const double e2 = __shfl_xor(be, o);
-    const int k2 = __shfl_xor(bk, o);
-    if (better(e2, k2, be, bk)) {
-      be = e2;
-      bk = k2;
-    }
+    const double e = __shfl_xor(b.be, o), w = __shfl_xor(b.bw, o), e2 = __shfl_xor(b.be2, o);
+    const int k = __shfl_xor(b.bk, o);
+    b.merge(e, k, w, e2);
   }
 }
 
@@ -376,12 +431,11 @@ __global__ void __launch_bounds__(256) scan_mid_kernel(Dev d, int pass) {
       u = d.mid[x];
       len = d.alen[u];
       if (len <= kMidLen) {
-        double be = -INFINITY;
-        int bk = INT_MAX;
-        scan_range(d, pass, u, lane, len, 64, be, bk);
-        wave_argmax(be, bk);
+        Top2 b;
+        scan_range(d, pass, u, lane, len, 64, b);
+        wave_argmax(b);
         if (lane == 0) {
-          scan_store(d, u, be, bk, prop);
+          scan_store(d, u, pass, b.be, b.bk, b.bw, b.be2, prop);
           d.late[u] = pass > 0;
           prop = prop && !d.touched[u];
         }
@@ -399,7 +453,7 @@ __global__ void __launch_bounds__(256) scan_mid_kernel(Dev d, int pass) {
 // one block per vertex of the big (T = 256) or huge (T = 1024) list
 template <int T>
 __global__ void __launch_bounds__(T) scan_big_kernel(Dev d, int pass) {
-  __shared__ double se[16];
+  __shared__ double se[16], sw[16], s2[16];
   __shared__ int sk[16];
   const int count = d.cnt[T == 1024 ? C_HUGE : C_BIG];
   const int* list = T == 1024 ? d.huge : d.big;
@@ -407,27 +461,104 @@ __global__ void __launch_bounds__(T) scan_big_kernel(Dev d, int pass) {
   for (int x = blockIdx.x; x < count; x += gridDim.x) {
     const int u = list[x];
     const int len = d.alen[u];
-    double be = -INFINITY;
-    int bk = INT_MAX;
-    scan_range(d, pass, u, tid, len, blockDim.x, be, bk);
-    wave_argmax(be, bk);
+    Top2 b;
+    scan_range(d, pass, u, tid, len, blockDim.x, b);
+    wave_argmax(b);
     if (lane_id() == 0) {
-      se[tid >> 6] = be;
-      sk[tid >> 6] = bk;
+      se[tid >> 6] = b.be;
+      sk[tid >> 6] = b.bk;
+      sw[tid >> 6] = b.bw;
+      s2[tid >> 6] = b.be2;
     }
     __syncthreads();
     if (tid < 64) {
-      be = tid < (int)(blockDim.x >> 6) ? se[tid] : -INFINITY;
-      bk = tid < (int)(blockDim.x >> 6) ? sk[tid] : INT_MAX;
-      wave_argmax(be, bk);
+      Top2 c;
+      if (tid < (int)(blockDim.x >> 6)) {
+        c.be = se[tid];
+        c.bk = sk[tid];
+        c.bw = sw[tid];
+        c.be2 = s2[tid];
+      }
+      wave_argmax(c);
       if (tid == 0) {
         bool prop;
-        scan_store(d, u, be, bk, prop);
+        scan_store(d, u, pass, c.be, c.bk, c.bw, c.be2, prop);
         d.late[u] = pass > 0;
         if (prop && !d.touched[u]) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
       }
     }
     __syncthreads();
+  }
+}
+
+// Lists longer than kBigLen (hubs: up to 652 K entries at C4): kHugeChunks
+// blocks per list, each scanning one contiguous chunk into a partial (argmax,
+// weight, runner-up) -- the order-free reduction of the same (eta desc, index
+// asc) total order -- and one wave per list combining the partials.
+struct HugePart {
+  double be, bw, be2;
+  int bk;
+};
+constexpr int kHugeChunks = 64;
+
+__global__ void __launch_bounds__(1024) scan_huge_part_kernel(Dev d, int pass, HugePart* part,
+                                                               int cap) {
+  __shared__ double se[16], sw[16], s2[16];
+  __shared__ int sk[16];
+  const int count = min(d.cnt[C_HUGE], cap);  // (cap: nnz / kBigLen + 2 > any count)
+  const int tid = threadIdx.x;
+  for (int li = blockIdx.y; li < count; li += gridDim.y) {
+    const int u = d.huge[li];
+    const long long len = d.alen[u];
+    const int b = (int)(len * blockIdx.x / kHugeChunks);
+    const int e = (int)(len * (blockIdx.x + 1) / kHugeChunks);
+    Top2 t;
+    scan_range(d, pass, u, b + tid, e, blockDim.x, t);
+    wave_argmax(t);
+    if (lane_id() == 0) {
+      se[tid >> 6] = t.be;
+      sk[tid >> 6] = t.bk;
+      sw[tid >> 6] = t.bw;
+      s2[tid >> 6] = t.be2;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      Top2 c;
+      if (tid < (int)(blockDim.x >> 6)) {
+        c.be = se[tid];
+        c.bk = sk[tid];
+        c.bw = sw[tid];
+        c.be2 = s2[tid];
+      }
+      wave_argmax(c);
+      if (tid == 0) part[(size_t)li * kHugeChunks + blockIdx.x] = HugePart{c.be, c.bw, c.be2, c.bk};
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) scan_huge_final_kernel(Dev d, int pass, const HugePart* part,
+                                                              int cap) {
+  const int count = min(d.cnt[C_HUGE], cap);
+  const int lane = lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  static_assert(kHugeChunks == 64, "one partial per lane");
+  for (int li = wave; li < count; li += nw) {
+    const HugePart h = part[(size_t)li * kHugeChunks + lane];
+    Top2 c;
+    c.be = h.be;
+    c.bw = h.bw;
+    c.be2 = h.be2;
+    c.bk = h.bk;
+    wave_argmax(c);
+    if (lane == 0) {
+      const int u = d.huge[li];
+      bool prop;
+      scan_store(d, u, pass, c.be, c.bk, c.bw, c.be2, prop);
+      d.late[u] = pass > 0;
+      if (prop && !d.touched[u]) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
+    }
   }
 }
 
@@ -1233,7 +1364,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DevBuf<unsigned long long> tops(2);  // [0] pool top, [1] global-table top
   DevBuf<int2> d_changes(n / 2 + 1);
   DevBuf<int2> pairs(kPairCap), pinfo(n);
-  DevBuf<int> pcnt(n), pbuf(kPairCap);
+  DevBuf<int> pcnt(n), pbuf(kPairCap), t2arg(n);
+  DevBuf<double> t2w(n), t2b2(n);
+  const int hcap = (int)(nnz / kBigLen + 2);  // lists longer than kBigLen: entries <= nnz
+  DevBuf<HugePart> hpart((size_t)hcap * kHugeChunks);
   GE_HIP(hipMemsetAsync(pcnt.p, 0, sizeof(int) * n, st));
 
   Dev d{};
@@ -1285,6 +1419,9 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d.pcnt = pcnt.p;
   d.pinfo = pinfo.p;
   d.pbuf = pbuf.p;
+  d.t2arg = t2arg.p;
+  d.t2w = t2w.p;
+  d.t2b2 = t2b2.p;
   d.patch = std::getenv("GE_PARTITION_NO_PATCH") == nullptr;
 
   note("buffers allocated");
@@ -1418,11 +1555,13 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       GE_HIP(hipMemsetAsync(cnt.p + C_SMALL, 0, sizeof(int) * 5, st));  // SMALL MID BIG PROP CAND
       GE_HIP(hipMemsetAsync(cnt.p + C_CAND2, 0, sizeof(int) * 2, st));  // CAND2 HUGE
       hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
-                         pass, alist_len, rounds, rounds == 1 ? 1 : 0);
+                         pass, alist_len, rounds, rounds == 1 ? 1 : 0, pass == matching - 1 ? 1 : 0);
       hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(scan_mid_kernel, dim3(mid_blocks), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(scan_big_kernel<256>, dim3(1024), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_big_kernel<1024>, dim3(256), dim3(1024), 0, st, d, pass);
+      hipLaunchKernelGGL(scan_huge_part_kernel, dim3(kHugeChunks, 64), dim3(1024), 0, st, d, pass,
+                         hpart.p, hcap);
+      hipLaunchKernelGGL(scan_huge_final_kernel, dim3(64), dim3(256), 0, st, d, pass, hpart.p, hcap);
       hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(resolve_min_kernel, dim3(512), dim3(256), 0, st, d);
       hipLaunchKernelGGL(resolve_select_kernel, dim3(512), dim3(256), 0, st, d, pass);
