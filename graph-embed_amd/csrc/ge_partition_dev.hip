@@ -69,6 +69,7 @@ constexpr int kPatchGone = 1024;
 constexpr int kPatchSet = 4096;
 constexpr int kPairCap = 1 << 22;
 constexpr int kPatchU = 16;
+constexpr int kSpecMerges = 4096;  // merge records copied with the round's counts
 
 enum {
   C_SMALL,
@@ -90,6 +91,12 @@ enum {
   C_PATCH,  // hub lists patched in place this round (profiling)
   C_PTOP,   // bucket space handed out to the hubs' absorbed-neighbour lists
   C_PF_SHORT, C_PF_SIZE, C_PF_FIT,  // lists rebuilt instead: short, sets too small, no room
+  // the per-pass and per-contraction counters are zeroed by the kernels that
+  // follow their last reader (no memset per round); their final values are kept
+  // here for the profile
+  C_SH_SMALL, C_SH_MID, C_SH_BIG, C_SH_PROP, C_SH_CAND, C_SH_HUGE,
+  C_SH_DIRTY, C_SH_W, C_SH_B, C_SH_G,
+  C_R_CHG, C_R_BOUND, C_R_PASS,  // rescans of lists > kSmallLen by reason (profile)
   NCNT
 };
 
@@ -153,7 +160,12 @@ struct Dev {
   int* t2arg;
   double* t2w;
   double* t2b2;
+  // ... and its runner-up (key, weight) with the best eta of the remaining entries
+  int* t2arg2;
+  double* t2w2;
+  double* t2b3;
   int patch;    // 0: every dirty list is rebuilt (GE_PARTITION_NO_PATCH)
+  int prof;     // GE_PROFILE_PARTITION: count rescans by reason
 };
 
 __device__ inline int lane_id() { return threadIdx.x & 63; }
@@ -222,43 +234,61 @@ __device__ inline double eta_of(const Dev& d, double w, double au, int k) {
   return 2.0 * (w / d.T - au * d.alpha[k]);  // :1715 (no contraction: -ffp-contract=off)
 }
 
-__device__ inline void scan_store(const Dev& d, int u, int pass, double be, int bk, double bw,
-                                  double be2, bool& prop) {
-  d.best[u] = be;
-  d.arg[u] = bk == INT_MAX ? -1 : bk;
-  prop = bk != INT_MAX && (!d.positive || be > 0.0);
-  if (pass == 0) {
-    d.t2arg[u] = bk == INT_MAX ? -1 : bk;
-    d.t2w[u] = bw;
-    d.t2b2[u] = be2;
-  }
-}
-
-// Running (argmax, its weight, best eta of the other entries) of a scan.
-struct Top2 {
-  double be = -INFINITY, bw = 0.0, be2 = -INFINITY;
-  int bk = INT_MAX;
+// Running (argmax, runner-up, best eta of the other entries) of a scan, under
+// the scan's total order (eta desc, index asc); merge() combines two partial
+// scans of disjoint entry sets.
+struct Top {
+  double be = -INFINITY, bw = 0.0, e2 = -INFINITY, w2 = 0.0, e3 = -INFINITY;
+  int bk = INT_MAX, k2 = INT_MAX;
   __device__ void add(double e, int k, double w) {
     if (better(e, k, be, bk)) {
-      be2 = fmax(be2, be);
+      e3 = fmax(e3, e2);
+      e2 = be;
+      k2 = bk;
+      w2 = bw;
       be = e;
       bk = k;
       bw = w;
+    } else if (better(e, k, e2, k2)) {
+      e3 = fmax(e3, e2);
+      e2 = e;
+      k2 = k;
+      w2 = w;
     } else {
-      be2 = fmax(be2, e);
+      e3 = fmax(e3, e);
     }
   }
-  __device__ void merge(double e, int k, double w, double e2) {  // another scan's state
-    if (better(e, k, be, bk)) {
-      be2 = fmax(fmax(be2, be), e2);
-      be = e;
-      bk = k;
-      bw = w;
-    } else {
-      be2 = fmax(be2, fmax(e, e2));
-    }
+  __device__ void merge(const Top& o) {
+    e3 = fmax(e3, o.e3);
+    add(o.be, o.bk, o.bw);
+    add(o.e2, o.k2, o.w2);
+  }
+  __device__ Top shfl_xor(int m) const {
+    Top o;
+    o.be = __shfl_xor(be, m);
+    o.bw = __shfl_xor(bw, m);
+    o.e2 = __shfl_xor(e2, m);
+    o.w2 = __shfl_xor(w2, m);
+    o.e3 = __shfl_xor(e3, m);
+    o.bk = __shfl_xor(bk, m);
+    o.k2 = __shfl_xor(k2, m);
+    return o;
   }
 };
+
+__device__ inline void scan_store(const Dev& d, int u, int pass, const Top& t, bool& prop) {
+  d.best[u] = t.be;
+  d.arg[u] = t.bk == INT_MAX ? -1 : t.bk;
+  prop = t.bk != INT_MAX && (!d.positive || t.be > 0.0);
+  if (pass == 0) {
+    d.t2arg[u] = t.bk == INT_MAX ? -1 : t.bk;
+    d.t2w[u] = t.bw;
+    d.t2b2[u] = fmax(t.e2, t.e3);
+    d.t2arg2[u] = t.k2 == INT_MAX ? -1 : t.k2;
+    d.t2w2[u] = t.w2;
+    d.t2b3[u] = t.e3;
+  }
+}
 
 // ---- scan (:1703-1726) -----------------------------------------------------
 // Which alive vertices the reference's scan would give a different answer than
@@ -278,13 +308,22 @@ struct Top2 {
 // proposer list; the rescans are split by list length.
 __global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full, int last) {
   __shared__ int s_app[6];
+  if (pass == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    // the previous contraction's counters (every reader has run) and the merge count
+    for (int q = 0; q < 4; ++q) {
+      d.cnt[C_SH_DIRTY + q] = d.cnt[C_DIRTY + q];  // DIRTY W B G
+      d.cnt[C_DIRTY + q] = 0;
+    }
+    *d.gtop = 0;
+    d.cnt[C_MERGE] = 0;
+  }
   const int stride = gridDim.x * blockDim.x;
   const int rounds = (L + stride - 1) / stride;
   for (int r = 0; r < rounds; ++r) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x + r * stride;
     int u = 0;
     bool resc = false, keepprop = false;
-    int len = 0;
+    int len = 0, why = 0;
     if (x < L) {
       u = d.alist[x];
       if (d.alive[u]) {
@@ -292,7 +331,9 @@ __global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full
         const int a = d.arg[u];
         if (pass == 0) {
           resc = full || !d.incremental || d.chg[u] == round - 1;
+          why = resc ? 1 : 0;
           if (!resc && (d.late[u] || (a >= 0 && d.kst[a] == round - 1))) {
+            why = 2;
             // The last pass-0 scan's argmax a0 may have lost eta (its alpha grew)
             // or been excluded since (late).  u's list and alpha are unchanged
             // since that scan (chg), and every other alpha only grew, so every
@@ -314,6 +355,21 @@ __global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full
           }
         } else if (!tu) {
           resc = !d.incremental || (a >= 0 && d.touched[a]);
+          why = 3;
+          const int k2 = d.t2arg2[u];
+          if (resc && d.incremental && a >= 0 && a == d.t2arg[u] && k2 >= 0 && !d.touched[k2]) {
+            // The argmax a of the last pass-0 scan is touched.  Every entry but a
+            // and its runner-up k2 has eta <= the b3 that scan recorded (the bound
+            // argument above), so if k2 is untouched and its eta now exceeds b3,
+            // k2 is the best untouched entry -- what the rescan returns.
+            const double e = eta_of(d, d.t2w2[u], d.alpha[u], k2);
+            if (e > d.t2b3[u]) {
+              d.best[u] = e;
+              d.arg[u] = k2;
+              d.late[u] = 1;
+              resc = false;
+            }
+          }
           if (resc && d.incremental && last && d.positive && a >= 0 && a == d.t2arg[u] &&
               d.t2b2[u] <= 0.0) {
             // The last pass under positiveMerging: every entry but a has eta <=
@@ -338,6 +394,13 @@ __global__ void classify_scan_kernel(Dev d, int pass, int L, int round, int full
     int* const ctrs[3] = {&d.cnt[C_SMALL], &d.cnt[C_MID], &d.cnt[C_PROP]};
     const bool pr[3] = {resc && len <= kSmallLen, resc && len > kSmallLen, keepprop};
     block_append<3>(lists, ctrs, pr, u, s_app);
+    if (d.prof) {
+#pragma unroll
+      for (int q = 1; q <= 3; ++q) {
+        const unsigned long long m = __ballot(resc && len > kSmallLen && why == q);
+        if (lane_id() == 0 && m) atomicAdd(&d.cnt[C_R_CHG + q - 1], __popcll(m));
+      }
+    }
   }
 }
 
@@ -354,7 +417,7 @@ __global__ void scan_small_kernel(Dev d, int pass) {
     if (x < count) {
       u = d.small[x];
       const int len = d.alen[u];
-      Top2 b;
+      Top b;
       const double au = d.alpha[u];
       const long long o = d.aoff[u];
       for (int t = 0; t < len; ++t) {
@@ -363,7 +426,7 @@ __global__ void scan_small_kernel(Dev d, int pass) {
         const double w = d.aw[o + t];
         b.add(eta_of(d, w, au, k), k, w);
       }
-      scan_store(d, u, pass, b.be, b.bk, b.bw, b.be2, prop);
+      scan_store(d, u, pass, b, prop);
       d.late[u] = pass > 0;
       prop = prop && !d.touched[u];
     }
@@ -376,7 +439,7 @@ __global__ void scan_small_kernel(Dev d, int pass) {
 
 // Scan entries [b, e) of u's list with `stride` cooperating threads, 4 in flight.
 __device__ inline void scan_range(const Dev& d, int pass, int u, int b, int e, int stride,
-                                  Top2& bt) {
+                                  Top& bt) {
   const double au = d.alpha[u];
   const long long o = d.aoff[u];
   int t = b;
@@ -408,13 +471,9 @@ __device__ inline void scan_range(const Dev& d, int pass, int u, int b, int e, i
   }
 }
 
-__device__ inline void wave_argmax(Top2& b) {
+__device__ inline void wave_argmax(Top& b) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double e = __shfl_xor(b.be, o), w = __shfl_xor(b.bw, o), e2 = __shfl_xor(b.be2, o);
-    const int k = __shfl_xor(b.bk, o);
-    b.merge(e, k, w, e2);
-  }
+  for (int o = 32; o > 0; o >>= 1) b.merge(b.shfl_xor(o));
 }
 
 // one wave per vertex of the mid list; longer lists go on to the big list
@@ -431,11 +490,11 @@ __global__ void __launch_bounds__(256) scan_mid_kernel(Dev d, int pass) {
       u = d.mid[x];
       len = d.alen[u];
       if (len <= kMidLen) {
-        Top2 b;
+        Top b;
         scan_range(d, pass, u, lane, len, 64, b);
         wave_argmax(b);
         if (lane == 0) {
-          scan_store(d, u, pass, b.be, b.bk, b.bw, b.be2, prop);
+          scan_store(d, u, pass, b, prop);
           d.late[u] = pass > 0;
           prop = prop && !d.touched[u];
         }
@@ -453,36 +512,26 @@ __global__ void __launch_bounds__(256) scan_mid_kernel(Dev d, int pass) {
 // one block per vertex of the big (T = 256) or huge (T = 1024) list
 template <int T>
 __global__ void __launch_bounds__(T) scan_big_kernel(Dev d, int pass) {
-  __shared__ double se[16], sw[16], s2[16];
-  __shared__ int sk[16];
+  __shared__ __attribute__((aligned(16))) char st_raw[16 * sizeof(Top)];  // (Top has initialisers)
+  Top* st = reinterpret_cast<Top*>(st_raw);
   const int count = d.cnt[T == 1024 ? C_HUGE : C_BIG];
   const int* list = T == 1024 ? d.huge : d.big;
   const int tid = threadIdx.x;
   for (int x = blockIdx.x; x < count; x += gridDim.x) {
     const int u = list[x];
     const int len = d.alen[u];
-    Top2 b;
+    Top b;
     scan_range(d, pass, u, tid, len, blockDim.x, b);
     wave_argmax(b);
-    if (lane_id() == 0) {
-      se[tid >> 6] = b.be;
-      sk[tid >> 6] = b.bk;
-      sw[tid >> 6] = b.bw;
-      s2[tid >> 6] = b.be2;
-    }
+    if (lane_id() == 0) st[tid >> 6] = b;
     __syncthreads();
     if (tid < 64) {
-      Top2 c;
-      if (tid < (int)(blockDim.x >> 6)) {
-        c.be = se[tid];
-        c.bk = sk[tid];
-        c.bw = sw[tid];
-        c.be2 = s2[tid];
-      }
+      Top c;
+      if (tid < (int)(blockDim.x >> 6)) c = st[tid];
       wave_argmax(c);
       if (tid == 0) {
         bool prop;
-        scan_store(d, u, pass, c.be, c.bk, c.bw, c.be2, prop);
+        scan_store(d, u, pass, c, prop);
         d.late[u] = pass > 0;
         if (prop && !d.touched[u]) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
       }
@@ -495,16 +544,12 @@ __global__ void __launch_bounds__(T) scan_big_kernel(Dev d, int pass) {
 // blocks per list, each scanning one contiguous chunk into a partial (argmax,
 // weight, runner-up) -- the order-free reduction of the same (eta desc, index
 // asc) total order -- and one wave per list combining the partials.
-struct HugePart {
-  double be, bw, be2;
-  int bk;
-};
 constexpr int kHugeChunks = 64;
 
-__global__ void __launch_bounds__(1024) scan_huge_part_kernel(Dev d, int pass, HugePart* part,
+__global__ void __launch_bounds__(1024) scan_huge_part_kernel(Dev d, int pass, Top* part,
                                                                int cap) {
-  __shared__ double se[16], sw[16], s2[16];
-  __shared__ int sk[16];
+  __shared__ __attribute__((aligned(16))) char st_raw[16 * sizeof(Top)];  // (Top has initialisers)
+  Top* st = reinterpret_cast<Top*>(st_raw);
   const int count = min(d.cnt[C_HUGE], cap);  // (cap: nnz / kBigLen + 2 > any count)
   const int tid = threadIdx.x;
   for (int li = blockIdx.y; li < count; li += gridDim.y) {
@@ -512,32 +557,22 @@ __global__ void __launch_bounds__(1024) scan_huge_part_kernel(Dev d, int pass, H
     const long long len = d.alen[u];
     const int b = (int)(len * blockIdx.x / kHugeChunks);
     const int e = (int)(len * (blockIdx.x + 1) / kHugeChunks);
-    Top2 t;
+    Top t;
     scan_range(d, pass, u, b + tid, e, blockDim.x, t);
     wave_argmax(t);
-    if (lane_id() == 0) {
-      se[tid >> 6] = t.be;
-      sk[tid >> 6] = t.bk;
-      sw[tid >> 6] = t.bw;
-      s2[tid >> 6] = t.be2;
-    }
+    if (lane_id() == 0) st[tid >> 6] = t;
     __syncthreads();
     if (tid < 64) {
-      Top2 c;
-      if (tid < (int)(blockDim.x >> 6)) {
-        c.be = se[tid];
-        c.bk = sk[tid];
-        c.bw = sw[tid];
-        c.be2 = s2[tid];
-      }
+      Top c;
+      if (tid < (int)(blockDim.x >> 6)) c = st[tid];
       wave_argmax(c);
-      if (tid == 0) part[(size_t)li * kHugeChunks + blockIdx.x] = HugePart{c.be, c.bw, c.be2, c.bk};
+      if (tid == 0) part[(size_t)li * kHugeChunks + blockIdx.x] = c;
     }
     __syncthreads();
   }
 }
 
-__global__ void __launch_bounds__(256) scan_huge_final_kernel(Dev d, int pass, const HugePart* part,
+__global__ void __launch_bounds__(256) scan_huge_final_kernel(Dev d, int pass, const Top* part,
                                                               int cap) {
   const int count = min(d.cnt[C_HUGE], cap);
   const int lane = lane_id();
@@ -545,17 +580,12 @@ __global__ void __launch_bounds__(256) scan_huge_final_kernel(Dev d, int pass, c
   const int nw = (gridDim.x * blockDim.x) >> 6;
   static_assert(kHugeChunks == 64, "one partial per lane");
   for (int li = wave; li < count; li += nw) {
-    const HugePart h = part[(size_t)li * kHugeChunks + lane];
-    Top2 c;
-    c.be = h.be;
-    c.bw = h.bw;
-    c.be2 = h.be2;
-    c.bk = h.bk;
+    Top c = part[(size_t)li * kHugeChunks + lane];
     wave_argmax(c);
     if (lane == 0) {
       const int u = d.huge[li];
       bool prop;
-      scan_store(d, u, pass, c.be, c.bk, c.bw, c.be2, prop);
+      scan_store(d, u, pass, c, prop);
       d.late[u] = pass > 0;
       if (prop && !d.touched[u]) d.prop[atomicAdd(&d.cnt[C_PROP], 1)] = u;
     }
@@ -661,7 +691,24 @@ constexpr int kLocalSlots = 4096;  // LDS phase: endpoint table (load <= 1/2)
 // Greedy matching in rank order via locally-dominant rounds; one block.  While
 // more than kLocalCand candidates are live the rounds run on global memory
 // (vertex-indexed lock array); the rest runs in LDS (endpoints hashed to slots).
+__device__ void resolve_block(Dev d, int pass, int cidx);
+
+// The matching's last kernel of a pass; then the pass's list counters are zeroed
+// for the next pass (every reader of them has run).
 __global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass, int cidx) {
+  resolve_block(d, pass, cidx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int from[6] = {C_SMALL, C_MID, C_BIG, C_PROP, C_CAND, C_HUGE};
+    for (int q = 0; q < 6; ++q) {
+      d.cnt[C_SH_SMALL + q] = d.cnt[from[q]];
+      d.cnt[from[q]] = 0;
+    }
+    d.cnt[C_CAND2] = 0;
+  }
+}
+
+__device__ void resolve_block(Dev d, int pass, int cidx) {
   __shared__ int s_live;
   __shared__ int hk[kLocalSlots];
   __shared__ int hl[kLocalSlots];
@@ -1364,10 +1411,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DevBuf<unsigned long long> tops(2);  // [0] pool top, [1] global-table top
   DevBuf<int2> d_changes(n / 2 + 1);
   DevBuf<int2> pairs(kPairCap), pinfo(n);
-  DevBuf<int> pcnt(n), pbuf(kPairCap), t2arg(n);
-  DevBuf<double> t2w(n), t2b2(n);
+  DevBuf<int> pcnt(n), pbuf(kPairCap), t2arg(n), t2arg2(n);
+  DevBuf<double> t2w(n), t2b2(n), t2w2(n), t2b3(n);
   const int hcap = (int)(nnz / kBigLen + 2);  // lists longer than kBigLen: entries <= nnz
-  DevBuf<HugePart> hpart((size_t)hcap * kHugeChunks);
+  DevBuf<Top> hpart((size_t)hcap * kHugeChunks);
   GE_HIP(hipMemsetAsync(pcnt.p, 0, sizeof(int) * n, st));
 
   Dev d{};
@@ -1422,7 +1469,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   d.t2arg = t2arg.p;
   d.t2w = t2w.p;
   d.t2b2 = t2b2.p;
+  d.t2arg2 = t2arg2.p;
+  d.t2w2 = t2w2.p;
+  d.t2b3 = t2b3.p;
   d.patch = std::getenv("GE_PARTITION_NO_PATCH") == nullptr;
+  d.prof = prof ? 1 : 0;
 
   note("buffers allocated");
   GE_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int) * NCNT, st));
@@ -1552,8 +1603,6 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     ++rounds;
     const auto t0 = now();
     for (int pass = 0; pass < matching; ++pass) {
-      GE_HIP(hipMemsetAsync(cnt.p + C_SMALL, 0, sizeof(int) * 5, st));  // SMALL MID BIG PROP CAND
-      GE_HIP(hipMemsetAsync(cnt.p + C_CAND2, 0, sizeof(int) * 2, st));  // CAND2 HUGE
       hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
                          pass, alist_len, rounds, rounds == 1 ? 1 : 0, pass == matching - 1 ? 1 : 0);
       hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
@@ -1574,22 +1623,27 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       if (prof) {  // per-pass list sizes (extra synchronisation: profiling only)
         GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
         GE_HIP(hipStreamSynchronize(st));
-        for (int c = C_SMALL; c <= C_CAND; ++c) stat[c] += h_cnt[c];
-        stat[C_HUGE] += h_cnt[C_HUGE];
-        for (int c : {(int)C_SMALL, (int)C_MID, (int)C_BIG, (int)C_HUGE, (int)C_PROP, (int)C_CAND})
-          rstat[c] += h_cnt[c];
+        // (resolve_kernel moved the pass's counts to the C_SH_* slots)
+        const int from[6] = {C_SMALL, C_MID, C_BIG, C_PROP, C_CAND, C_HUGE};
+        for (int q = 0; q < 6; ++q) {
+          stat[from[q]] += h_cnt[C_SH_SMALL + q];
+          rstat[from[q]] += h_cnt[C_SH_SMALL + q];
+        }
       }
     }
     GE_HIP(hipGetLastError());
     GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
     GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    // the merge records of a typical round come with the counts (one synchronisation)
+    const int spec = std::min(kSpecMerges, n / 2 + 1);
+    GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * spec, hipMemcpyDeviceToHost, st));
     GE_HIP(hipStreamSynchronize(st));
     if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
     if (prof) {
-      for (int c = C_DIRTY; c <= C_G; ++c) {
-        stat[c] += h_cnt[c];  // previous round's contraction
-        rstat[c] = h_cnt[c];
+      for (int q = 0; q < 4; ++q) {  // previous round's contraction (DIRTY W B G)
+        stat[C_DIRTY + q] += h_cnt[C_SH_DIRTY + q];
+        rstat[C_DIRTY + q] = h_cnt[C_SH_DIRTY + q];
       }
       for (int c : {(int)C_PATCH, (int)C_PF_SHORT, (int)C_PF_SIZE, (int)C_PF_FIT}) {
         rstat[c] = h_cnt[c] - (int)stat[c];  // these counters accumulate
@@ -1602,8 +1656,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                                                   : "partition_device: list pool overflow");
     const int nm = rb.merges;
     if (nm > 0) {
-      GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * nm, hipMemcpyDeviceToHost, st));
-      GE_HIP(hipStreamSynchronize(st));
+      if (nm > spec) {
+        GE_HIP(hipMemcpyAsync(h_mrec + spec, mrec.p + spec, sizeof(MergeRec) * (nm - spec),
+                              hipMemcpyDeviceToHost, st));
+        GE_HIP(hipStreamSynchronize(st));
+      }
       // fresh pool space this round needs at most 1.5 x (both lists) + 4 per keeper
       long long worst = 0;
       for (int x = 0; x < nm; ++x)
@@ -1635,8 +1692,6 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       }
       // contraction on the device (asynchronous) while the host does the
       // order-dependent bookkeeping
-      GE_HIP(hipMemsetAsync(cnt.p + C_DIRTY, 0, sizeof(int) * 4, st));  // DIRTY W B G
-      GE_HIP(hipMemsetAsync(tops.p + 1, 0, sizeof(unsigned long long), st));
       hipLaunchKernelGGL(merge_apply_kernel, dim3(blocks_for(nm, 256)), dim3(256), 0, st, d, rounds);
       hipLaunchKernelGGL(mark_dirty_kernel, dim3(blocks_for(nm, 4)), dim3(256), 0, st, d);
       hipLaunchKernelGGL(classify_kernel, dim3(1024), dim3(256), 0, st, d);
@@ -1645,7 +1700,6 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       hipLaunchKernelGGL(rebuild_block_kernel, dim3(1024), dim3(256), 0, st, d);
       hipLaunchKernelGGL(rebuild_global_kernel, dim3(256), dim3(1024), 0, st, d);
       hipLaunchKernelGGL(dirty_reset_kernel, dim3(1024), dim3(256), 0, st, d, rounds);
-      GE_HIP(hipMemsetAsync(cnt.p + C_MERGE, 0, sizeof(int), st));
       GE_HIP(hipGetLastError());
       if (rounds <= 2 && progress) {  // profiling the first rounds: wait for the contraction
         GE_HIP(hipStreamSynchronize(st));
@@ -1731,6 +1785,11 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                  stat[C_DIRTY],
                  stat[C_W], stat[C_B], stat[C_G], stat[C_PATCH], stat[C_PF_SHORT], stat[C_PF_SIZE],
                  stat[C_PF_FIT]);
+  if (prof)
+    std::fprintf(stderr,
+                 "partition_device rescans of lists > %d entries by reason: changed %d, bound "
+                 "failed %d, argmax touched %d\n",
+                 kSmallLen, h_cnt[C_R_CHG], h_cnt[C_R_BOUND], h_cnt[C_R_PASS]);
   if (printing) {  // :1880-1889
     std::cout << "modularity: " << Q << std::endl;
     std::cout << "level 0: " << n << " aggregates" << std::endl;
