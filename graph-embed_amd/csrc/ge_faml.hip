@@ -32,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "ge_internal.hpp"
@@ -724,9 +725,13 @@ struct ge_faml_plan {
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
   // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters
   bool sym = false;
+  bool sym_pair = false;  // faml_sym_pair (one wave per block, two row tiles per unit)
   ge::DevBuf<int4> units;
   ge::DevBuf<int> prog;
   int nunits = 0, ntiles = 0, sym_blocks = 0;
+  std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
+  ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
+  std::string stamp_path;
   double streamed_pairs = 0.0;
   ge::DevBuf<double> Fscr, Fprev, Xa, Xb, DP;
   // the size classes are independent: streamed path, large, mid and small
@@ -898,17 +903,27 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::vector<int> T(big.size());
     const bool any_big = !big.empty();
     for (size_t b = 0; b < big.size(); ++b) T[b] = (h_pt_ip[big[b] + 1] - h_pt_ip[big[b]] + 63) / 64;
+    {
+      // two row tiles per wave (faml_sym_pair): bit-exact, but slower at C4 (139.8
+      // against 152.9 ms per launch: more units in flight spin longer), so opt-in
+      const char* e = std::getenv("GE_FAML_SYM_PAIR");
+      pl->sym_pair = e && *e == '1';
+    }
+    const int sym_threads = pl->sym_pair ? 64 : kSymT;
     int occ = 1;
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
+          &occ, pl->sym_pair ? (const void*)faml_sym_pair<D, false>
+                             : (const void*)faml_sym_repulse<D, false>,
+          sym_threads, 0));
     });
-    int bpc = std::min(std::max(occ, 1), 4);
+    int bpc = std::min(std::max(occ, 1), pl->sym_pair ? 16 : 4);
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
-    const double waves = (double)pl->sym_blocks * (kSymT / 64);
+    // a pair unit carries two row tiles: count its wave twice in the model
+    const double waves = (double)pl->sym_blocks * (sym_threads / 64) * (pl->sym_pair ? 2 : 1);
     std::vector<size_t> by_T(big.size());
     std::iota(by_T.begin(), by_T.end(), 0);
     std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
@@ -965,9 +980,25 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     struct Unit { int a, A, pb, T, kind; double est; };
     std::vector<Unit> us;
     int pb = 0;
+    // Queue position of sweep A of an aggregate of T row tiles: 2A Tmax / T, i.e.
+    // every aggregate's sweeps spread over the whole queue, so all aggregates reach
+    // their last (chain-bound) sweeps together and the launch ends without a tail of
+    // the largest aggregate's chain (C4: tail after the queue drained 8.7 -> 3.5 ms,
+    // 148.1 -> 143.2 ms per launch).  GE_FAML_SYM_PROP=0: 2A, the sweep's earliest
+    // start (diagnostics; GE_FAML_SYM_EST scales the 2).
+    double est_k = 2.0;
+    if (const char* e = std::getenv("GE_FAML_SYM_EST")) est_k = std::atof(e);
+    const bool est_prop = !(std::getenv("GE_FAML_SYM_PROP") && *std::getenv("GE_FAML_SYM_PROP") == '0');
+    const int Tmax = big.empty() ? 1 : *std::max_element(T.begin(), T.end());
+    auto est_of = [&](int A, int Tb) { return est_k * A * (est_prop ? (double)Tmax / Tb : 1.0); };
     for (size_t b = 0; b < big.size(); ++b) {
       if (rows_mode[b]) continue;
-      for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], 0, 2.0 * A});
+      if (pl->sym_pair) {  // row tiles (A, A + 1); a last odd tile with an inert second
+        for (int A = 0; A < T[b]; A += 2)
+          us.push_back({big[b], A, pb, T[b], 2, est_of(A, T[b])});
+      } else {
+        for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], 0, est_of(A, T[b])});
+      }
       pb += T[b];
     }
     std::vector<Unit> rows_units;
@@ -996,6 +1027,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     pl->ntiles = pb;
     pl->units.alloc(h_units.size());
     pl->units.upload(h_units.data(), h_units.size(), st);
+    if (const char* e = std::getenv("GE_SYM_STAMPS")) {  // diagnostics: timeline of each launch
+      pl->stamp_path = e;
+      pl->h_units = h_units;
+      pl->stamps.alloc(h_units.size() * kStampWords);
+    }
     pl->prog.alloc(std::max(pb, 1));
   }
   pl->R = R;
@@ -1134,14 +1170,32 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
         }
         if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
-          if (c.repel == 1.0)
+          if (pl->sym_pair) {
+            if (!pl->stamp_path.empty())
+              hipLaunchKernelGGL((faml_sym_pair<D, false, true>), dim3(pl->sym_blocks), dim3(64),
+                                 0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, pl->stamps.p);
+            else if (c.repel == 1.0)
+              hipLaunchKernelGGL((faml_sym_pair<D, true>), dim3(pl->sym_blocks), dim3(64), 0, ss,
+                                 pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
+            else
+              hipLaunchKernelGGL((faml_sym_pair<D, false>), dim3(pl->sym_blocks), dim3(64), 0, ss,
+                                 pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
+          } else if (!pl->stamp_path.empty())
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
+                               dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
+                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p,
+                               pl->stamps.p);
+          else if (c.repel == 1.0)
             hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
                                ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
           else
             hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSymT), 0,
                                ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p);
+                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                                 pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
@@ -1195,6 +1249,18 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     GE_HIP(hipStreamWaitEvent(st, pl->join[0], 0));
   });
   GE_HIP(hipGetLastError());
+  if (!pl->stamp_path.empty() && pl->nunits > 0) {  // the last launch's timeline
+    std::vector<long long> h((size_t)pl->nunits * kStampWords);
+    GE_HIP(hipStreamSynchronize(st));
+    GE_HIP(hipMemcpy(h.data(), pl->stamps.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    if (FILE* f = std::fopen(pl->stamp_path.c_str(), "wb")) {
+      const int hdr[4] = {pl->nunits, kStampWords, pl->sym_blocks, pl->sym_pair ? 64 : kSymT};
+      std::fwrite(hdr, sizeof(int), 4, f);
+      std::fwrite(pl->h_units.data(), sizeof(int4), pl->h_units.size(), f);
+      std::fwrite(h.data(), sizeof(long long), h.size(), f);
+      std::fclose(f);
+    }
+  }
 }
 
 static void faml_plan_free(ge_faml_plan* pl) {

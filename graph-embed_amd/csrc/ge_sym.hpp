@@ -149,9 +149,9 @@ __device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, c
 }
 
 // Column tile t of the sweep has left lane 63: write its sums back, then let the
-// next sweep of the aggregate have it.
+// next sweep of the aggregate have it (tprog[t] = done: row tiles < done added).
 template <int D>
-__device__ __forceinline__ void sym_handover(int t, int lane, int A, int ncols, size_t cbase,
+__device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncols, size_t cbase,
                                              const double* out, double* F, int* tprog) {
   constexpr int IW = SymI<D>::v;
   wave_lds_sync();
@@ -169,7 +169,7 @@ __device__ __forceinline__ void sym_handover(int t, int lane, int A, int ncols, 
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0);  // every lane's sums are stored before the flag
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  if (lane == 0) __hip_atomic_store(tprog + t, A + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_store(tprog + t, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D, bool REPEL_ONE, bool DIAG>
@@ -231,16 +231,130 @@ __device__ __forceinline__ void rows_block(int lane, int base, int s, int A, con
   wave_lds_sync();
 }
 
+// Per-unit timeline of one launch (STAMP builds only, GE_SYM_STAMPS): 8 words per
+// unit in queue order -- s_memrealtime (100 MHz, one clock for the whole chip)
+// when the wave took the unit, when its first column tile was handed over, when it
+// finished, the ticks spent spinning on hand-overs, HW_ID and XCC_ID.
+constexpr int kStampWords = 8;
+
+__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+
+// One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
+// column sums handed to the next sweep tile by tile.  rec / ini / out: this wave's
+// rings (kSymRing slots each).  STAMP: spin ticks and the first hand-over time.
+template <int D, bool REPEL_ONE, bool STAMP>
+__device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
+                                           const double* __restrict__ X,
+                                           const double* __restrict__ DP, double repel,
+                                           bool repel_ok, double* __restrict__ F, double* rec,
+                                           double* ini, double* out, long long& spin,
+                                           long long& t_first) {
+  constexpr int IW = SymI<D>::v;
+  const size_t cbase = (size_t)base + 64 * (size_t)A;
+  const bool rv = 64 * A + lane < s;
+  double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
+    racc[k] = 0.0;
+    flow[k] = 0.0;
+  }
+  if (rv) dr = DP[cbase + lane];
+  const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
+  const int ncols = s - 64 * A;
+  const int ntiles = (ncols + 63) >> 6;
+  bool ok_prev = true;
+  for (int tt = 0; tt < ntiles; ++tt) {
+    if (A > 0) {  // the sweeps 0..A-1 have written column tile A + tt back
+      const long long t0 = STAMP ? rt_now() : 0;
+      while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
+        __builtin_amdgcn_s_sleep(1);
+      if (STAMP) {
+        const long long t1 = rt_now();
+        spin += t1 - t0;
+        if (tt == 0) t_first = t1;
+      }
+      // the F loads below are agent-scope (served past the L2) and issued only after
+      // the spin has seen the flag (the loop's exit depends on the loaded value); the
+      // fence keeps the compiler from hoisting them above the loop
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    const int qc = 64 * tt + lane;
+    const bool cv = qc < ncols;
+    double xc[D], ic[D], dc = 0.0;  // a column past the aggregate is inert
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
+      ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
+    }
+    if (cv) dc = DP[cbase + qc];
+    const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
+    double* rs = rec + (qc & (kSymRing - 1));
+    double* is = ini + (qc & (kSymRing - 1)) * IW;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      rs[k * kSymRing] = xc[k];
+      is[k] = ic[k];
+    }
+    rs[D * kSymRing] = dc;
+    wave_lds_sync();
+    // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
+    const bool fast = rows_ok && ok_cur && ok_prev;
+    if (tt < 2)
+      sym_steps_any<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini, out,
+                                        xr, dr, rv, repel, racc, flow);
+    else
+      sym_steps_any<D, REPEL_ONE, false>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini,
+                                         out, xr, dr, rv, repel, racc, flow);
+    ok_prev = ok_cur;
+    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, out, F, tprog);
+    wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
+  }
+  {  // drain: the last columns cross the wave; the slots past them hold inert records
+    double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1));
+    double* is = ini + ((64 * ntiles + lane) & (kSymRing - 1)) * IW;
+#pragma unroll
+    for (int k = 0; k <= D; ++k) rs[k * kSymRing] = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) is[k] = 0.0;
+    wave_lds_sync();
+  }
+  const int s0 = 64 * ntiles, s1 = ncols + 63;
+  if (ntiles < 2)
+    sym_steps_any<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
+                                      xr, dr, rv, repel, racc, flow);
+  else
+    sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
+                                       xr, dr, rv, repel, racc, flow);
+  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, F, tprog);
+  if (rv) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
+  }
+}
+
+// Stamp record of one unit (STAMP builds): see kStampWords.
+__device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long t_take,
+                                           long long t_first, long long spin) {
+  long long* w = stamps + (size_t)qi * kStampWords;
+  w[0] = t_take;
+  w[1] = t_first;
+  w[2] = rt_now();
+  w[3] = spin;
+  w[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+  w[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+}
+
 // units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
 // kind (0: symmetric sweep, 1: row block)} in queue order; prog zeroed before the
 // launch; queue = one counter.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3)
-template <int D, bool REPEL_ONE>
+template <int D, bool REPEL_ONE, bool STAMP = false>
 __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
-                 int* __restrict__ prog) {
+                 int* __restrict__ prog, long long* __restrict__ stamps) {
   constexpr int WV = SymW<D>::v;
   constexpr int IW = SymI<D>::v;
   constexpr int NW = kSymT / 64;
@@ -257,6 +371,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     if (lane == 0) qi = atomicAdd(queue, 1);
     qi = __builtin_amdgcn_readfirstlane(qi);
     if (qi >= nunits) break;  // every wave leaves once the queue is drained
+    long long t_take = 0, t_first = 0, spin = 0;
+    if (STAMP) t_take = t_first = rt_now();
     const int4 u = units[qi];
     const int A = u.y;
     const int base = pt_ip[u.x];
@@ -267,84 +383,251 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
-      continue;
+    } else {
+      sweep_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel, repel_ok,
+                                      F, rec, ini, out, spin, t_first);
     }
-    int* tprog = prog + u.z + A;  // tprog[t]: column tile A + t
-    const size_t cbase = (size_t)base + 64 * (size_t)A;
-    const bool rv = 64 * A + lane < s;
-    double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
+    if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
+    wave_lds_sync();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pair sweeps (faml_sym_pair): one wave carries the sweeps of row tiles A and
+// A+1 as two systolic streams.  Stream b runs 128 steps behind stream a, so the
+// sum of column q leaves a's lane 63 exactly one step before it has to enter b's
+// lane 0 (a wave rotate moves it there); b's lane 63 stores each finished column
+// sum to F.  Per column, rows of tile A then rows of tile A+1 in ascending order:
+// the order of two consecutive single sweeps, so the same bits.  The two streams
+// are independent instruction chains (twice the work between waits), the column
+// records are staged once for both, and only every second row tile hands its
+// column tiles over.  An aggregate with an odd tile count ends with a pair whose
+// stream b rows are all past the aggregate (inert: its terms are +-0).
+//
+// Stream a at step tau, lane l: (row 64A + l, column tau - l); stream b: (row
+// 64(A+1) + l, column tau - 64 - l) (columns relative to 64A).  Records: a ring
+// of four column tiles (stream a reads tiles tt-1 and tt during global tile tt,
+// stream b tiles tt-2 and tt-1).  Column C leaves stream b at step C + 127, so
+// column tile K is complete after global tile K + 2 (K >= 2: tiles 0 and 1 are
+// the pair's own rows).  LDS: 9.5 KB per wave at D = 3 (four waves per SIMD).
+
+constexpr int kPairRec = 256;  // record slots per component (4 column tiles)
+constexpr int kPairIni = 64;   // entering column sums of stream a (the current tile)
+
+template <int D>
+constexpr int pair_arena_doubles() {
+  const int pair = (D + 1) * kPairRec + kPairIni * SymI<D>::v;
+  const int rows = 64 * SymW<D>::v;
+  return pair > rows ? pair : rows;
+}
+
+// Wave rotate by one lane (DPP wave_ror:1): lane l receives lane l-1, lane 0 lane 63.
+__device__ __forceinline__ double wave_ror1(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x13C, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x13C, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// STORE: b's lane 63 stores the column leaving it (tau >= 255, i.e. columns >= 128).
+template <int D, bool SHARED, bool REPEL_ONE, bool DIAG_A, bool DIAG_B, bool STORE>
+__device__ __forceinline__ void pair_step(int tau, int lane, const double* rec, const double* ini,
+                                          double* Fc, const double (&xa)[D], double da,
+                                          const double (&xb)[D], double db, double repel,
+                                          double (&racc_a)[D], double (&flow_a)[D],
+                                          double (&racc_b)[D], double (&flow_b)[D]) {
+  constexpr int IW = SymI<D>::v;
+  const double* ic = ini + (tau & (kPairIni - 1)) * IW;
+  const int sa = (tau - lane) & (kPairRec - 1);
+  const int sb = (tau - 64 - lane) & (kPairRec - 1);
+  double ia[D], ra[D + 1], rb[D + 1];
+#pragma unroll
+  for (int k = 0; k < D; ++k) ia[k] = ic[k];
+#pragma unroll
+  for (int k = 0; k <= D; ++k) {
+    ra[k] = rec[k * kPairRec + sa];
+    rb[k] = rec[k * kPairRec + sb];
+  }
+  // b's entering column is the sum that left a's lane 63 at the previous step;
+  // column tau enters a's lane 0 with its stored sum
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    flow_b[k] = wave_ror1(lane == 63 ? flow_a[k] : flow_b[k]);
+    flow_a[k] = wave_shift_in(flow_a[k], ia[k]);
+  }
+  const bool diag_a = DIAG_A && tau - lane == lane;
+  const bool diag_b = DIAG_B && tau - 128 - lane == lane;
+  if (diag_a)
+#pragma unroll
+    for (int k = 0; k < D; ++k) racc_a[k] = flow_a[k];
+  if (diag_b)
+#pragma unroll
+    for (int k = 0; k < D; ++k) racc_b[k] = flow_b[k];
+  double ta[D], tb[D];
+  rep_term<D, SHARED, REPEL_ONE>(xa, ra, da, ra[D], repel, ta);
+  rep_term<D, SHARED, REPEL_ONE>(xb, rb, db, rb[D], repel, tb);
+  if (!SHARED && (diag_a || diag_b)) {  // the `/` form skips the self pair (ge_pair.hpp)
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
-      racc[k] = 0.0;
-      flow[k] = 0.0;
+      if (diag_a) ta[k] = 0.0;
+      if (diag_b) tb[k] = 0.0;
     }
-    if (rv) dr = DP[cbase + lane];
-    const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
-    const int ncols = s - 64 * A;
-    const int ntiles = (ncols + 63) >> 6;
-    bool ok_prev = true;
-    for (int tt = 0; tt < ntiles; ++tt) {
-      if (A > 0) {  // the sweeps 0..A-1 have written column tile A + tt back
-        while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
-          __builtin_amdgcn_s_sleep(1);
-        // the F loads below are agent-scope (served past the L2) and issued only after
-        // the spin has seen the flag (the loop's exit depends on the loaded value); the
-        // fence keeps the compiler from hoisting them above the loop
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    racc_a[k] = racc_a[k] + ta[k];
+    flow_a[k] = flow_a[k] - ta[k];
+    racc_b[k] = racc_b[k] + tb[k];
+    flow_b[k] = flow_b[k] - tb[k];
+  }
+  if (STORE && lane == 63) {  // column tau - 127 leaves stream b: its sum is final here
+    double* o = Fc + (size_t)(tau - 127) * D;
+#pragma unroll
+    for (int k = 0; k < D; ++k) agent_st(o + k, flow_b[k]);
+  }
+}
+
+template <int D, bool REPEL_ONE, bool DIAG_A, bool DIAG_B, bool STORE>
+__device__ __forceinline__ void pair_steps(bool fast, int t0, int t1, int lane, const double* rec,
+                                           const double* ini, double* Fc, const double (&xa)[D],
+                                           double da, const double (&xb)[D], double db,
+                                           double repel, double (&racc_a)[D], double (&flow_a)[D],
+                                           double (&racc_b)[D], double (&flow_b)[D]) {
+  if (fast) {
+    for (int tau = t0; tau < t1; ++tau)
+      pair_step<D, true, REPEL_ONE, DIAG_A, DIAG_B, STORE>(tau, lane, rec, ini, Fc, xa, da, xb,
+                                                           db, repel, racc_a, flow_a, racc_b,
+                                                           flow_b);
+  } else {
+    for (int tau = t0; tau < t1; ++tau)
+      pair_step<D, false, REPEL_ONE, DIAG_A, DIAG_B, STORE>(tau, lane, rec, ini, Fc, xa, da, xb,
+                                                            db, repel, racc_a, flow_a, racc_b,
+                                                            flow_b);
+  }
+}
+
+template <int D, bool REPEL_ONE, bool STAMP>
+__device__ __forceinline__ void pair_unit(int lane, int A, int base, int s, int* tprog,
+                                          const double* __restrict__ X,
+                                          const double* __restrict__ DP, double repel,
+                                          bool repel_ok, double* __restrict__ F, double* rec,
+                                          double* ini, long long& spin, long long& t_first) {
+  constexpr int IW = SymI<D>::v;
+  const size_t cbase = (size_t)base + 64 * (size_t)A;
+  double* Fc = F + cbase * D;
+  const bool rva = 64 * A + lane < s, rvb = 64 * A + 64 + lane < s;
+  double xa[D], xb[D], racc_a[D], flow_a[D], racc_b[D], flow_b[D], da = 0.0, db = 0.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {  // rows past the aggregate are inert
+    xa[k] = rva ? X[(cbase + lane) * D + k] : 0.0;
+    xb[k] = rvb ? X[(cbase + 64 + lane) * D + k] : 0.0;
+    racc_a[k] = flow_a[k] = racc_b[k] = flow_b[k] = 0.0;
+  }
+  if (rva) da = DP[cbase + lane];
+  if (rvb) db = DP[cbase + 64 + lane];
+  const bool rows_ok =
+      repel_ok && __all((!rva || vertex_ok<D>(xa, da)) && (!rvb || vertex_ok<D>(xb, db)));
+  const int ncols = s - 64 * A;
+  const int ntiles = (ncols + 63) >> 6;
+  const int tau_end = ncols + 127;  // the last column leaves stream b at step ncols + 126
+  bool ok1 = true, ok2 = true;      // column tiles tt-1 and tt-2 in the exact domain
+  for (int tt = 0; tt <= ntiles + 1; ++tt) {
+    const int qc = 64 * tt + lane;
+    const bool cv = qc < ncols;  // tiles past the aggregate stage inert records
+    if (A > 0 && tt < ntiles) {  // the units before have written column tile A + tt back
+      const long long t0 = STAMP ? rt_now() : 0;
+      while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
+        __builtin_amdgcn_s_sleep(1);
+      if (STAMP) {
+        const long long t1 = rt_now();
+        spin += t1 - t0;
+        if (tt == 0) t_first = t1;
       }
-      const int qc = 64 * tt + lane;
-      const bool cv = qc < ncols;
-      double xc[D], ic[D], dc = 0.0;  // a column past the aggregate is inert
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
-        ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
-      }
-      if (cv) dc = DP[cbase + qc];
-      const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
-      double* rs = rec + (qc & (kSymRing - 1));
-      double* is = ini + (qc & (kSymRing - 1)) * IW;
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        rs[k * kSymRing] = xc[k];
-        is[k] = ic[k];
-      }
-      rs[D * kSymRing] = dc;
-      wave_lds_sync();
-      // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
-      const bool fast = rows_ok && ok_cur && ok_prev;
-      if (tt < 2)
-        sym_steps_any<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini, out,
-                                          xr, dr, rv, repel, racc, flow);
-      else
-        sym_steps_any<D, REPEL_ONE, false>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini,
-                                           out, xr, dr, rv, repel, racc, flow);
-      ok_prev = ok_cur;
-      if (tt >= 2) sym_handover<D>(tt - 1, lane, A, ncols, cbase, out, F, tprog);
-      wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // as in sweep_unit
     }
-    {  // drain: the last columns cross the wave; the slots past them hold inert records
-      double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1));
-      double* is = ini + ((64 * ntiles + lane) & (kSymRing - 1)) * IW;
+    double xc[D], ic[D], dc = 0.0;
 #pragma unroll
-      for (int k = 0; k <= D; ++k) rs[k * kSymRing] = 0.0;
-#pragma unroll
-      for (int k = 0; k < D; ++k) is[k] = 0.0;
-      wave_lds_sync();
+    for (int k = 0; k < D; ++k) {
+      xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
+      ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
     }
-    const int s0 = 64 * ntiles, s1 = ncols + 63;
-    if (ntiles < 2)
-      sym_steps_any<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
-                                        xr, dr, rv, repel, racc, flow);
-    else
-      sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
-                                         xr, dr, rv, repel, racc, flow);
-    if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A, ncols, cbase, out, F, tprog);
-    if (rv) {
+    if (cv) dc = DP[cbase + qc];
+    const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
+    double* rs = rec + (qc & (kPairRec - 1));
+    double* is = ini + (qc & (kPairIni - 1)) * IW;
 #pragma unroll
-      for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
+    for (int k = 0; k < D; ++k) {
+      rs[k * kPairRec] = xc[k];
+      is[k] = ic[k];
     }
+    rs[D * kPairRec] = dc;
+    wave_lds_sync();
+    const bool fast = rows_ok && ok_cur && ok1 && ok2;
+    const int t0 = 64 * tt, t1 = min(64 * tt + 64, tau_end);
+    if (tt < 2) {  // a's diagonal tile (b has not started: its lanes hold dead values)
+      pair_steps<D, REPEL_ONE, true, false, false>(fast, t0, t1, lane, rec, ini, Fc, xa, da, xb,
+                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
+    } else if (tt < 4) {  // b's diagonal tile; column 128 leaves b at the last step of tile 3
+      const int t1s = min(t1, 255);
+      pair_steps<D, REPEL_ONE, false, true, false>(fast, t0, t1s, lane, rec, ini, Fc, xa, da, xb,
+                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
+      pair_steps<D, REPEL_ONE, false, true, true>(fast, t1s, t1, lane, rec, ini, Fc, xa, da, xb,
+                                                  db, repel, racc_a, flow_a, racc_b, flow_b);
+    } else {
+      pair_steps<D, REPEL_ONE, false, false, true>(fast, t0, t1, lane, rec, ini, Fc, xa, da, xb,
+                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
+    }
+    ok2 = ok1;
+    ok1 = ok_cur;
+    if (tt >= 4 && tt - 2 < ntiles) {
+      // column tile tt - 2 is in F: every store of it has completed (s_waitcnt 0)
+      // before the flag (see sym_handover)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_waitcnt(0);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane == 0)
+        __hip_atomic_store(tprog + tt - 2, A + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    wave_lds_sync();  // the slots staged next are free
+  }
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    if (rva) F[(cbase + lane) * D + k] = racc_a[k];
+    if (rvb) F[(cbase + 64 + lane) * D + k] = racc_b[k];
+  }
+}
+
+// One wave per block; units of kind 2 (pairs; the last of an aggregate with an odd
+// tile count has an inert stream b) and 1 (row blocks).
+// 4 waves per SIMD: <= 128 VGPRs
+template <int D, bool REPEL_ONE, bool STAMP = false>
+__global__ void __launch_bounds__(64, 4)
+faml_sym_pair(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
+              const int* __restrict__ pt_ip, const double* __restrict__ X,
+              const double* __restrict__ DP, double repel, double* __restrict__ F,
+              int* __restrict__ prog, long long* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) double arena[pair_arena_doubles<D>()];
+  const int lane = threadIdx.x;
+  const bool repel_ok = REPEL_ONE || weight_ok(repel);
+  for (;;) {
+    int qi = 0;
+    if (lane == 0) qi = atomicAdd(queue, 1);
+    qi = __builtin_amdgcn_readfirstlane(qi);
+    if (qi >= nunits) break;  // every wave leaves once the queue is drained
+    long long t_take = 0, t_first = 0, spin = 0;
+    if (STAMP) t_take = t_first = rt_now();
+    const int4 u = units[qi];
+    const int A = u.y;
+    const int base = pt_ip[u.x];
+    const int s = pt_ip[u.x + 1] - base;
+    if (u.w == 1) {
+      __builtin_amdgcn_s_setprio(3);  // as in faml_sym_repulse
+      rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, arena, F);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      pair_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel, repel_ok, F,
+                                     arena, arena + (D + 1) * kPairRec, spin, t_first);
+    }
+    if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
   }
 }

@@ -468,6 +468,31 @@ def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("pair,dim,repel", [
+    ("1", 3, 1.0), ("1", 3, 2.0 ** 70), ("1", 2, 1.5), ("1", 4, 1.0), ("0", 3, 1.0),
+    ("0", 3, 2.0 ** 70)])
+def test_faml_symmetric_pairs(ctx, oracle, monkeypatch, pair, dim, repel):
+    """faml_sym_pair (ge_sym.hpp): two row tiles per wave (stream b 128 steps
+    behind stream a), the hand-over every second row tile; even and odd tile
+    counts (the odd one ends with a single sweep), ragged last tiles, one-member
+    last tiles, last pairs of two tiles (no hand-over), hub rows; against the oracle
+    and against the one-tile-per-wave kernel (pair = 0)."""
+    monkeypatch.setenv("GE_FAML_SYM", "1")
+    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "0")
+    monkeypatch.setenv("GE_FAML_SYM_PAIR", pair)
+    sizes = [2560, 383, 704, 257, 1089, 300, 448, 90, 1, 4100]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=13), [(5, 2500), (2600, 3000)], seed=dim)
+    PT = _block_partition(n, sizes, seed=7)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m + 1)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=23, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=23, repel=repel)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("dim", [2, 4])
 def test_faml_dims(ctx, oracle, dim):
     A = G.largest_component(G.rmat(1500, 9000, seed=dim))
