@@ -918,7 +918,10 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
                              : (const void*)faml_sym_repulse<D, false>,
           sym_threads, 0));
     });
-    int bpc = std::min(std::max(occ, 1), pl->sym_pair ? 16 : 4);
+    // three blocks (waves) per SIMD of the four that fit: fewer units in flight spin
+    // less on hand-overs (C4 N = 1: 137.2 against 138.3 ms per launch; N = 8 shares
+    // 30.0 against 32.7 ms; scripts/sym_timeline.py, profiles/r03/sym_timeline)
+    int bpc = std::min(std::max(occ, 1), pl->sym_pair ? 16 : 3);
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
@@ -1183,7 +1186,12 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
               hipLaunchKernelGGL((faml_sym_pair<D, false>), dim3(pl->sym_blocks), dim3(64), 0, ss,
                                  pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
                                  pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
-          } else if (!pl->stamp_path.empty())
+          } else if (!pl->stamp_path.empty() && std::getenv("GE_SYM_NOWAIT"))  // timing only
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
+                               dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
+                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p,
+                               pl->stamps.p);
+          else if (!pl->stamp_path.empty())
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p,

@@ -642,14 +642,41 @@ __device__ inline void record_merge(const Dev& d, int i, int j, int r, int pass)
 
 // The first locally-dominant round over the whole grid (most candidates of a
 // late round are leaves pointing at the same hub: one round removes them).
-__global__ void resolve_min_kernel(Dev d) {
+// lk[v] = the smallest rank of the candidates touching v.  Most candidates of a
+// late round propose to one of a few hubs (C4 round 2490: 371 679 candidates, 98
+// merges), so the hub endpoints' minima are first taken in a per-block LDS table
+// (keyed by vertex, open addressing over kMinSlots) and each table entry then
+// makes one global atomicMin: the same minima with far fewer contended atomics.
+// The proposer's own lock (distinct per candidate) goes straight to global.
+constexpr int kMinSlots = 512;
+__global__ void __launch_bounds__(256) resolve_min_kernel(Dev d) {
+  __shared__ int s_key[kMinSlots];
+  __shared__ int s_min[kMinSlots];
+  for (int q = threadIdx.x; q < kMinSlots; q += blockDim.x) {
+    s_key[q] = -1;
+    s_min[q] = kNone;
+  }
+  __syncthreads();
   const int n = d.cnt[C_CAND];
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const int i = d.cand[c];
+    const int j = d.arg[i];
     const int r = d.rank[i];
     atomicMin(&d.lk[i], r);
-    atomicMin(&d.lk[d.arg[i]], r);
+    bool done = false;
+    int h = (int)(((unsigned)j * 2654435761u) >> 23) & (kMinSlots - 1);
+    for (int probe = 0; probe < 8 && !done; ++probe, h = (h + 1) & (kMinSlots - 1)) {
+      const int k = atomicCAS(&s_key[h], -1, j);
+      if (k == -1 || k == j) {
+        atomicMin(&s_min[h], r);
+        done = true;
+      }
+    }
+    if (!done) atomicMin(&d.lk[j], r);  // table crowded: directly
   }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kMinSlots; q += blockDim.x)
+    if (s_key[q] >= 0) atomicMin(&d.lk[s_key[q]], s_min[q]);
 }
 
 __global__ void resolve_select_kernel(Dev d, int pass) {

@@ -242,7 +242,7 @@ __device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdg
 // One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
 // column sums handed to the next sweep tile by tile.  rec / ini / out: this wave's
 // rings (kSymRing slots each).  STAMP: spin ticks and the first hand-over time.
-template <int D, bool REPEL_ONE, bool STAMP>
+template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false>
 __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
                                            const double* __restrict__ X,
                                            const double* __restrict__ DP, double repel,
@@ -265,7 +265,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   const int ntiles = (ncols + 63) >> 6;
   bool ok_prev = true;
   for (int tt = 0; tt < ntiles; ++tt) {
-    if (A > 0) {  // the sweeps 0..A-1 have written column tile A + tt back
+    if (A > 0 && !NOWAIT) {  // the sweeps 0..A-1 have written column tile A + tt back
       const long long t0 = STAMP ? rt_now() : 0;
       while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
         __builtin_amdgcn_s_sleep(1);
@@ -348,8 +348,9 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
 // units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
 // kind (0: symmetric sweep, 1: row block)} in queue order; prog zeroed before the
 // launch; queue = one counter.
-// 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3)
-template <int D, bool REPEL_ONE, bool STAMP = false>
+// 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
+// (diagnostics, wrong results): no sweep waits for its hand-overs.
+template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
 __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
@@ -384,8 +385,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
     } else {
-      sweep_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel, repel_ok,
-                                      F, rec, ini, out, spin, t_first);
+      sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
+                                              repel_ok, F, rec, ini, out, spin, t_first);
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
