@@ -3,7 +3,7 @@
 # the same command, FETCH / WRITE PMC passes restricted to the dominant kernel.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r02final}
+TAG=${1:-r03final}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
