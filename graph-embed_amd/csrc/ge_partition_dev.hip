@@ -1278,6 +1278,25 @@ __global__ void rank_update_kernel(Dev d, int count, const int2* __restrict__ ch
   if (x < count) d.rank[ch[x].x] = ch[x].y;
 }
 
+// The round's counters, pool top and first `spec` merge records written straight
+// into pinned host memory (one launch instead of three blit copies, each of which
+// waited ~15 us behind the last kernel).  System-scope vector stores; the stream
+// synchronisation that follows completes the kernel and its release before the
+// host reads them.
+__global__ void __launch_bounds__(256) export_round_kernel(Dev d, const unsigned long long* __restrict__ tops,
+                                                           int* __restrict__ hcnt,
+                                                           unsigned long long* __restrict__ htop,
+                                                           int* __restrict__ hrec, int spec) {
+  const int t = threadIdx.x;
+  for (int c = t; c < NCNT; c += blockDim.x)
+    __hip_atomic_store(&hcnt[c], d.cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) __hip_atomic_store(htop, tops[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int nw = min(d.cnt[C_MERGE], spec) * (int)(sizeof(MergeRec) / sizeof(int));
+  const int* src = reinterpret_cast<const int*>(d.mrec);
+  for (int w = t; w < nw; w += blockDim.x)
+    __hip_atomic_store(&hrec[w], src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ---- set-up ------------------------------------------------------------------
 // Eligibility (rows strictly ascending -> no duplicate keys; integer weights;
 // A symmetric with equal weights) and the lists: row i minus its diagonal
@@ -1616,6 +1635,9 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   int alist_len = n;
   int mid_blocks = 1024;  // GE_PART_MID_BLOCKS: tuning
   if (const char* e = std::getenv("GE_PART_MID_BLOCKS")) mid_blocks = std::max(1, std::atoi(e));
+  // GE_PART_BLIT_EXPORT=1: the round's counts and records by three blit copies
+  // (the earlier path, for comparison) instead of export_round_kernel
+  const bool blit_export = std::getenv("GE_PART_BLIT_EXPORT") != nullptr;
   double t_dev = 0, t_host = 0, t_compact = 0;
   long long total_merges = 0;
   int rounds = 0, compactions = 0;
@@ -1658,12 +1680,17 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         }
       }
     }
-    GE_HIP(hipGetLastError());
-    GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
-    GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     // the merge records of a typical round come with the counts (one synchronisation)
     const int spec = std::min(kSpecMerges, n / 2 + 1);
-    GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * spec, hipMemcpyDeviceToHost, st));
+    if (blit_export) {
+      GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
+      GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+      GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * spec, hipMemcpyDeviceToHost, st));
+    } else {
+      hipLaunchKernelGGL(export_round_kernel, dim3(1), dim3(256), 0, st, d, tops.p, h_cnt, h_top,
+                         reinterpret_cast<int*>(h_mrec), spec);
+    }
+    GE_HIP(hipGetLastError());
     GE_HIP(hipStreamSynchronize(st));
     if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
@@ -1766,9 +1793,15 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     for (int x = 0; x < nch; ++x) h_changes[x] = make_int2(moved[x], pointer[moved[x]]);
     total_merges += nm;
     if (nch > 0) {
-      GE_HIP(hipMemcpyAsync(d_changes.p, h_changes, sizeof(int2) * nch, hipMemcpyHostToDevice, st));
+      // the kernel reads the pinned changes directly (no H2D blit); the host next
+      // writes h_changes after the next round's synchronisation, past this kernel
+      const int2* chg = h_changes;
+      if (blit_export) {
+        GE_HIP(hipMemcpyAsync(d_changes.p, h_changes, sizeof(int2) * nch, hipMemcpyHostToDevice, st));
+        chg = d_changes.p;
+      }
       hipLaunchKernelGGL(rank_update_kernel, dim3(blocks_for(nch, 256)), dim3(256), 0, st, d, nch,
-                         d_changes.p);
+                         chg);
       GE_HIP(hipGetLastError());
     }
     if (alist_len > M + M / 4 + 1024) {  // drop the dead entries of the alive list

@@ -11,8 +11,8 @@ from collections import defaultdict
 
 
 def short(nm):
-    nm = nm.split("(")[0]
-    return nm.replace("ge::(anonymous namespace)::", "").replace("void ", "")
+    nm = nm.replace("ge::(anonymous namespace)::", "").replace("void ", "")
+    return nm.split("(")[0]
 
 
 rows = []
