@@ -720,9 +720,34 @@ constexpr int kLocalSlots = 4096;  // LDS phase: endpoint table (load <= 1/2)
 // (vertex-indexed lock array); the rest runs in LDS (endpoints hashed to slots).
 __device__ void resolve_block(Dev d, int pass, int cidx);
 
+// The round's counters, pool top and first `spec` merge records written straight
+// into pinned host memory by the round's last kernel (no blit copies, each of
+// which waited ~15 us behind the last kernel).  System-scope vector stores; the
+// stream synchronisation that follows completes the kernel and its release before
+// the host reads them.
+struct RoundExport {
+  const unsigned long long* tops = nullptr;
+  int* hcnt = nullptr;  // nullptr: not the round's last pass
+  unsigned long long* htop = nullptr;
+  int* hrec = nullptr;
+  int spec = 0;
+};
+
+__device__ void export_round(const Dev& d, const RoundExport& ex) {
+  const int t = threadIdx.x;
+  for (int c = t; c < NCNT; c += blockDim.x)
+    __hip_atomic_store(&ex.hcnt[c], d.cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 0) __hip_atomic_store(ex.htop, ex.tops[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int nw = min(d.cnt[C_MERGE], ex.spec) * (int)(sizeof(MergeRec) / sizeof(int));
+  const int* src = reinterpret_cast<const int*>(d.mrec);
+  for (int w = t; w < nw; w += blockDim.x)
+    __hip_atomic_store(&ex.hrec[w], src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The matching's last kernel of a pass; then the pass's list counters are zeroed
-// for the next pass (every reader of them has run).
-__global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass, int cidx) {
+// for the next pass (every reader of them has run).  The round's last pass also
+// exports the round (ex.hcnt set).
+__global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass, int cidx, RoundExport ex) {
   resolve_block(d, pass, cidx);
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -732,6 +757,10 @@ __global__ void __launch_bounds__(1024) resolve_kernel(Dev d, int pass, int cidx
       d.cnt[from[q]] = 0;
     }
     d.cnt[C_CAND2] = 0;
+  }
+  if (ex.hcnt) {
+    __syncthreads();  // the merge records and the moved counters are complete
+    export_round(d, ex);
   }
 }
 
@@ -1278,24 +1307,6 @@ __global__ void rank_update_kernel(Dev d, int count, const int2* __restrict__ ch
   if (x < count) d.rank[ch[x].x] = ch[x].y;
 }
 
-// The round's counters, pool top and first `spec` merge records written straight
-// into pinned host memory (one launch instead of three blit copies, each of which
-// waited ~15 us behind the last kernel).  System-scope vector stores; the stream
-// synchronisation that follows completes the kernel and its release before the
-// host reads them.
-__global__ void __launch_bounds__(256) export_round_kernel(Dev d, const unsigned long long* __restrict__ tops,
-                                                           int* __restrict__ hcnt,
-                                                           unsigned long long* __restrict__ htop,
-                                                           int* __restrict__ hrec, int spec) {
-  const int t = threadIdx.x;
-  for (int c = t; c < NCNT; c += blockDim.x)
-    __hip_atomic_store(&hcnt[c], d.cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (t == 0) __hip_atomic_store(htop, tops[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const int nw = min(d.cnt[C_MERGE], spec) * (int)(sizeof(MergeRec) / sizeof(int));
-  const int* src = reinterpret_cast<const int*>(d.mrec);
-  for (int w = t; w < nw; w += blockDim.x)
-    __hip_atomic_store(&hrec[w], src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // ---- set-up ------------------------------------------------------------------
 // Eligibility (rows strictly ascending -> no duplicate keys; integer weights;
@@ -1636,8 +1647,9 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   int mid_blocks = 1024;  // GE_PART_MID_BLOCKS: tuning
   if (const char* e = std::getenv("GE_PART_MID_BLOCKS")) mid_blocks = std::max(1, std::atoi(e));
   // GE_PART_BLIT_EXPORT=1: the round's counts and records by three blit copies
-  // (the earlier path, for comparison) instead of export_round_kernel
+  // (the earlier path, for comparison) instead of the export by the last resolve_kernel
   const bool blit_export = std::getenv("GE_PART_BLIT_EXPORT") != nullptr;
+  const int spec = std::min(kSpecMerges, n / 2 + 1);
   double t_dev = 0, t_host = 0, t_compact = 0;
   long long total_merges = 0;
   int rounds = 0, compactions = 0;
@@ -1667,7 +1679,15 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       {
         Dev d2 = d;  // the survivors are in cand2
         std::swap(d2.cand, d2.cand2);
-        hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d2, pass, (int)C_CAND2);
+        RoundExport ex;  // the round's last pass exports its counts and records
+        if (pass == matching - 1 && !blit_export) {
+          ex.tops = tops.p;
+          ex.hcnt = h_cnt;
+          ex.htop = h_top;
+          ex.hrec = reinterpret_cast<int*>(h_mrec);
+          ex.spec = spec;
+        }
+        hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d2, pass, (int)C_CAND2, ex);
       }
       if (prof) {  // per-pass list sizes (extra synchronisation: profiling only)
         GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
@@ -1681,14 +1701,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       }
     }
     // the merge records of a typical round come with the counts (one synchronisation)
-    const int spec = std::min(kSpecMerges, n / 2 + 1);
     if (blit_export) {
       GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
       GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
       GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * spec, hipMemcpyDeviceToHost, st));
-    } else {
-      hipLaunchKernelGGL(export_round_kernel, dim3(1), dim3(256), 0, st, d, tops.p, h_cnt, h_top,
-                         reinterpret_cast<int*>(h_mrec), spec);
     }
     GE_HIP(hipGetLastError());
     GE_HIP(hipStreamSynchronize(st));
