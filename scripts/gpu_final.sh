@@ -3,7 +3,7 @@
 # the same command, FETCH / WRITE PMC passes restricted to the dominant kernel.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r03final2}
+TAG=${1:-r03final3}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
