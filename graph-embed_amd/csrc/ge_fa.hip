@@ -1042,9 +1042,15 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   const int grp = blockIdx.x / kBarGroup;
   const int members = min(kBarGroup, nb - grp * kBarGroup);
   int* gc = bar + kBarLine * (2 + grp);
-  const int old = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // Release / acquire at agent scope (the HIP memory model, not only the store
+  // completion the callers' s_waitcnt gives): the arrival releases this block's
+  // coordinate stores (ordered before it by the block's __syncthreads), the group's
+  // last arrival acquires its group's releases and releases them on to the grid
+  // counter, and a waiter acquires with one fence after its relaxed poll.  Once per
+  // iteration, so the L2 write-back / invalidate it implies costs little.
+  const int old = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   if (old == members * (it + 1) - 1)  // the group's last arrival
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
   const int target = ngroups * (it + 1);
   const long long t0 = wall_clock64();
   while (coh_ldi(cnt) < target) {
@@ -1054,6 +1060,7 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
@@ -1541,11 +1548,15 @@ static void plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, d
 
 // All iterations of a small level (n <= grouped_cap, every row) in one launch of
 // fa_grouped_persistent.  The grid must fit the device at half its block
-// occupancy (so a co-running kernel cannot keep part of it from becoming
-// resident): the lanes per row halve from grouped_lanes(n) until it does.
-// Returns false (nothing launched) when no G fits; GE_PERSIST_REQUIRE=1 (tests)
-// makes that an error.  The result is in Xa for an even iteration count, in Xb
-// for an odd one.
+// occupancy: the lanes per row halve from grouped_lanes(n) until it does.  The
+// launch is cooperative, so the runtime either makes the whole grid resident or
+// refuses it.  Other work on the device (another rank's persistent kernel on the
+// same GPU, another process) can still delay blocks past the barrier's ~2 s
+// bound: then the start state (coordinates, previous forces) is restored and the
+// caller runs the per-iteration path from it.  Returns false (nothing computed)
+// when no G fits, the launch is refused or the barrier timed out;
+// GE_PERSIST_REQUIRE=1 (tests) makes each of these an error.  The result is in
+// Xa for an even iteration count, in Xb for an odd one.
 constexpr int kPersistMin = 128;  // fewer iterations: per-iteration launches
 template <int D>
 bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
@@ -1553,8 +1564,12 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
   if (n > grouped_cap(D) || pl->rb != 0 || pl->re != n) return false;
   hipStream_t s = pl->ctx->stream;
   const size_t lds = grouped_lds_bytes(n, D);
-  bool launched = false, fits = false;
+  bool launched = false, fits = false, refused = false;
   DevBuf<int> bar;
+  // the start state, restored when the barrier times out
+  DevBuf<double> x0((size_t)n * D), f0((size_t)n * D);
+  GE_HIP(hipMemcpyAsync(x0.p, Xa, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+  GE_HIP(hipMemcpyAsync(f0.p, pl->fprev.p, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
   auto go = [&](auto GG) {
     constexpr int GC = decltype(GG)::value;
     const int nb = (n + kGrpT / GC - 1) / (kGrpT / GC);
@@ -1573,10 +1588,24 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
       const long long limit = (long long)std::max(khz, 1000) * 2000;  // ~2 s per barrier
       bar.alloc(persist_bar_ints(nb));
       GE_HIP(hipMemsetAsync(bar.p, 0, sizeof(int) * bar.n, s));
-      hipLaunchKernelGGL((fa_grouped_persistent<D, GC, R1, LIN>), dim3(nb), dim3(kGrpT), lds, s,
-                         n, pl->ip, pl->ix, pl->dx, Xa, Xb, pl->dp1.p, pl->c, pl->fprev.p, bar.p,
-                         iterations, limit);
-      GE_HIP(hipGetLastError());
+      int n_ = n, it_ = iterations;
+      long long lim_ = limit;
+      const int* ip_ = pl->ip;
+      const int* ix_ = pl->ix;
+      const double* dx_ = pl->dx;
+      const double* dp_ = pl->dp1.p;
+      FaConst c_ = pl->c;
+      double* fp_ = pl->fprev.p;
+      int* bar_ = bar.p;
+      void* args[] = {&n_, &ip_, &ix_, &dx_, &Xa, &Xb, &dp_, &c_, &fp_, &bar_, &it_, &lim_};
+      const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(nb), dim3(kGrpT), args,
+                                                      (unsigned)lds, s);
+      if (e == hipErrorCooperativeLaunchTooLarge) {
+        (void)hipGetLastError();
+        refused = true;
+        return;
+      }
+      GE_HIP(e);
       launched = true;
     };
     const bool lin = !pl->c.linlog && pl->c.delta == 1.0;
@@ -1601,16 +1630,28 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
       default: go(std::integral_constant<int, 1>()); break;
     }
   }
+  const char* req = std::getenv("GE_PERSIST_REQUIRE");
+  const bool require = req && *req == '1';
   if (!launched) {
-    if (const char* e = std::getenv("GE_PERSIST_REQUIRE"))
-      if (*e == '1') throw Error(GE_ERR_STATE, "forceAtlas: the persistent kernel does not fit");
+    if (require)
+      throw Error(GE_ERR_STATE, refused ? "forceAtlas: the cooperative launch was refused"
+                                        : "forceAtlas: the persistent kernel does not fit");
     return false;
   }
   int err = 0;
   GE_HIP(hipMemcpyAsync(&err, bar.p + 1, sizeof(int), hipMemcpyDeviceToHost, s));
   GE_HIP(hipStreamSynchronize(s));
-  if (err)
-    throw Error(GE_ERR_STATE, "forceAtlas: the persistent small-level kernel's grid barrier timed out");
+  if (err) {
+    if (require)
+      throw Error(GE_ERR_STATE,
+                  "forceAtlas: the persistent small-level kernel's grid barrier timed out");
+    std::fprintf(stderr, "libge: the persistent coarsest-level kernel's grid barrier timed out "
+                         "(device shared?); rerunning per iteration\n");
+    GE_HIP(hipMemcpyAsync(Xa, x0.p, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+    GE_HIP(hipMemcpyAsync(pl->fprev.p, f0.p, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+    GE_HIP(hipStreamSynchronize(s));
+    return false;
+  }
   return true;
 }
 

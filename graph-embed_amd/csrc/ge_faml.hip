@@ -728,6 +728,9 @@ struct ge_faml_plan {
   bool sym_pair = false;  // faml_sym_pair (one wave per block, two row tiles per unit)
   ge::DevBuf<int4> units;
   ge::DevBuf<int> prog;
+  ge::DevBuf<double> hand;  // column sums handed between sweeps, component-major [dim][n]
+  ge::DevBuf<int> sym_err;  // set by a hand-over wait that timed out
+  long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
@@ -870,6 +873,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     pl->ecls.bind(pl->erows.p);
     pl->rstreams.attach(pl->ecls, pl->dim, st, hdeg);
   }
+  // split tiles are one-row-slot items (R = 1): settle R before any item is built,
+  // so the whole-aggregate items step by the R the kernel is launched with
+  for (int a : split) {
+    int t0, t1;
+    tiles_of(a, rank, t0, t1);
+    if (t1 > t0) R = 1;
+  }
   struct Item { int a, r0; double work; };
   std::vector<Item> its;
   for (int a : big) {
@@ -881,7 +891,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     const int s = h_pt_ip[a + 1] - h_pt_ip[a];
     int t0, t1;
     tiles_of(a, rank, t0, t1);
-    if (t1 > t0) R = 1;
     for (int t = t0; t < t1; ++t) its.push_back({a, 64 * t, (double)s});
   }
   std::stable_sort(its.begin(), its.end(),
@@ -1036,6 +1045,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       pl->stamps.alloc(h_units.size() * kStampWords);
     }
     pl->prog.alloc(std::max(pb, 1));
+    if (pb > 0) pl->hand.alloc((size_t)pl->n * dim);
+    pl->sym_err.alloc(1);
+    GE_HIP(hipMemsetAsync(pl->sym_err.p, 0, sizeof(int), st));
+    int khz = 0;
+    GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    // one hand-over normally waits at most a few tile-times (tens of microseconds)
+    pl->sym_limit = (long long)std::max(khz, 1000) * 5000;  // ~5 s
   }
   pl->R = R;
   pl->code = big_code(R, U);
@@ -1173,37 +1189,51 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
         }
         if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
+          double* H = pl->hand.p;
+          const size_t hs = (size_t)pl->n;
+          int* err = pl->sym_err.p;
+          const long long lim = pl->sym_limit;
           if (pl->sym_pair) {
             if (!pl->stamp_path.empty())
               hipLaunchKernelGGL((faml_sym_pair<D, false, true>), dim3(pl->sym_blocks), dim3(64),
                                  0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, pl->stamps.p);
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim,
+                                 pl->stamps.p);
             else if (c.repel == 1.0)
               hipLaunchKernelGGL((faml_sym_pair<D, true>), dim3(pl->sym_blocks), dim3(64), 0, ss,
                                  pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim, nullptr);
             else
               hipLaunchKernelGGL((faml_sym_pair<D, false>), dim3(pl->sym_blocks), dim3(64), 0, ss,
                                  pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
-          } else if (!pl->stamp_path.empty() && std::getenv("GE_SYM_NOWAIT"))  // timing only
+                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim, nullptr);
+#ifdef GE_SYM_DIAGNOSTICS
+          } else if (!pl->stamp_path.empty() && std::getenv("GE_SYM_NOWAIT")) {
+            // timing only, WRONG results: no sweep waits for its hand-overs.  Built
+            // only with -DGE_SYM_DIAGNOSTICS (scripts/build_variant.sh NAME -DGE_SYM_DIAGNOSTICS), never in the
+            // shipped library.
+            std::fprintf(stderr, "libge: GE_SYM_NOWAIT diagnostics build: results are invalid\n");
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
-                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p,
-                               pl->stamps.p);
-          else if (!pl->stamp_path.empty())
+                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
+                               err, lim, pl->stamps.p);
+#endif
+          } else if (!pl->stamp_path.empty()) {
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
-                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p,
-                               pl->stamps.p);
-          else if (c.repel == 1.0)
+                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
+                               err, lim, pl->stamps.p);
+          } else if (c.repel == 1.0) {
             hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
                                ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
-          else
+                               pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p, err, lim,
+                               nullptr);
+          } else {
             hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSymT), 0,
                                ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, nullptr);
+                               pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p, err, lim,
+                               nullptr);
+          }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
                                 pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p);
@@ -1257,6 +1287,16 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     GE_HIP(hipStreamWaitEvent(st, pl->join[0], 0));
   });
   GE_HIP(hipGetLastError());
+  if (pl->sym && pl->nunits > 0) {  // a hand-over wait that timed out fails the call
+    int err = 0;
+    GE_HIP(hipMemcpyAsync(&err, pl->sym_err.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    GE_HIP(hipStreamSynchronize(st));
+    if (err) {
+      GE_HIP(hipMemsetAsync(pl->sym_err.p, 0, sizeof(int), st));
+      throw Error(GE_ERR_STATE,
+                  "forceAtlasMultilevel: a symmetric sweep's hand-over wait timed out");
+    }
+  }
   if (!pl->stamp_path.empty() && pl->nunits > 0) {  // the last launch's timeline
     std::vector<long long> h((size_t)pl->nunits * kStampWords);
     GE_HIP(hipStreamSynchronize(st));

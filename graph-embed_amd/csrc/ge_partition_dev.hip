@@ -1721,9 +1721,10 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       }
     }
     rb.top = *h_top;
+    if (h_cnt[C_OVF] == 2)  // a bug, not a capacity limit: never retried on the host
+      throw Error(GE_ERR_STATE, "partition_device: resolve did not converge");
     if (h_cnt[C_OVF])
-      throw Error(GE_ERR_STATE, h_cnt[C_OVF] == 2 ? "partition_device: resolve did not converge"
-                                                  : "partition_device: list pool overflow");
+      throw Error(GE_ERR_CAPACITY, "partition_device: list pool overflow");
     const int nm = rb.merges;
     if (nm > 0) {
       if (nm > spec) {
@@ -1757,7 +1758,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         d.akey = nkey;
         d.aw = nwt;
         if ((long long)*h_top + worst > pool_cap)
-          throw Error(GE_ERR_STATE, "partition_device: list pool exhausted after compaction");
+          throw Error(GE_ERR_CAPACITY, "partition_device: list pool exhausted after compaction");
         t_compact += secs(tc, now());
       }
       // contraction on the device (asynchronous) while the host does the

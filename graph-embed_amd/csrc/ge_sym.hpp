@@ -62,6 +62,8 @@ __device__ __forceinline__ void agent_st(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+
 constexpr int kSymRing = 128;  // LDS ring of column slots (column q at q & 127)
 
 template <int D>
@@ -150,16 +152,20 @@ __device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, c
 
 // Column tile t of the sweep has left lane 63: write its sums back, then let the
 // next sweep of the aggregate have it (tprog[t] = done: row tiles < done added).
+// The hand-over buffer H is component-major (H[k * hs + c]): each of the D store
+// instructions covers 512 contiguous bytes (8 lines) instead of the 24 lines a
+// 24-byte-strided record store spans, which the agent-scope stores pay per line.
 template <int D>
 __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncols, size_t cbase,
-                                             const double* out, double* F, int* tprog) {
+                                             const double* out, double* H, size_t hs,
+                                             int* tprog) {
   constexpr int IW = SymI<D>::v;
   wave_lds_sync();
   const int qo = 64 * t + lane;
   if (qo < ncols) {
     const double* o = out + (qo & (kSymRing - 1)) * IW;
 #pragma unroll
-    for (int k = 0; k < D; ++k) agent_st(F + (cbase + qo) * D + k, o[k]);
+    for (int k = 0; k < D; ++k) agent_st(H + k * hs + cbase + qo, o[k]);
   }
   // Ordering (no acquire/release: an agent-scope release would write back the whole
   // L2, ~every 64 steps): the sums are agent-scope stores (they bypass the per-XCD
@@ -170,6 +176,30 @@ __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncol
   __builtin_amdgcn_s_waitcnt(0);  // every lane's sums are stored before the flag
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   if (lane == 0) __hip_atomic_store(tprog + t, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until a column tile's progress counter reaches A.  Bounded: a wait longer
+// than `limit` ticks of the 100 MHz clock, or one another wave already reported
+// in *err, sets *err and gives up for the rest of the launch, so a scheduling bug
+// ends the launch (with wrong sums and an error the host reports) instead of
+// hanging the device.  Returns the ticks spent when STAMP.
+template <bool STAMP>
+__device__ __forceinline__ long long handover_wait(const int* flag, int A, int* err,
+                                                   long long limit, bool& give_up) {
+  if (give_up) return 0;
+  if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A) return 0;
+  const long long t0 = rt_now();
+  for (int k = 1;; ++k) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A) break;
+    if ((k & 255) == 0 &&
+        (rt_now() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      give_up = true;
+      break;
+    }
+  }
+  return STAMP ? rt_now() - t0 : 0;
 }
 
 template <int D, bool REPEL_ONE, bool DIAG>
@@ -237,7 +267,6 @@ __device__ __forceinline__ void rows_block(int lane, int base, int s, int A, con
 // finished, the ticks spent spinning on hand-overs, HW_ID and XCC_ID.
 constexpr int kStampWords = 8;
 
-__device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
 // One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
 // column sums handed to the next sweep tile by tile.  rec / ini / out: this wave's
@@ -246,7 +275,9 @@ template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false>
 __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
                                            const double* __restrict__ X,
                                            const double* __restrict__ DP, double repel,
-                                           bool repel_ok, double* __restrict__ F, double* rec,
+                                           bool repel_ok, double* __restrict__ F,
+                                           double* __restrict__ H, size_t hs, int* err,
+                                           long long limit, bool& give_up, double* rec,
                                            double* ini, double* out, long long& spin,
                                            long long& t_first) {
   constexpr int IW = SymI<D>::v;
@@ -266,13 +297,10 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   bool ok_prev = true;
   for (int tt = 0; tt < ntiles; ++tt) {
     if (A > 0 && !NOWAIT) {  // the sweeps 0..A-1 have written column tile A + tt back
-      const long long t0 = STAMP ? rt_now() : 0;
-      while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
-        __builtin_amdgcn_s_sleep(1);
+      const long long w = handover_wait<STAMP>(tprog + tt, A, err, limit, give_up);
       if (STAMP) {
-        const long long t1 = rt_now();
-        spin += t1 - t0;
-        if (tt == 0) t_first = t1;
+        spin += w;
+        if (tt == 0) t_first = rt_now();
       }
       // the F loads below are agent-scope (served past the L2) and issued only after
       // the spin has seen the flag (the loop's exit depends on the loaded value); the
@@ -285,7 +313,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
-      ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
+      ic[k] = (cv && A > 0) ? agent_ld(H + k * hs + cbase + qc) : 0.0;
     }
     if (cv) dc = DP[cbase + qc];
     const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
@@ -307,7 +335,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
       sym_steps_any<D, REPEL_ONE, false>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini,
                                          out, xr, dr, rv, repel, racc, flow);
     ok_prev = ok_cur;
-    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, out, F, tprog);
+    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
     wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
   }
   {  // drain: the last columns cross the wave; the slots past them hold inert records
@@ -326,7 +354,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   else
     sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
                                        xr, dr, rv, repel, racc, flow);
-  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, F, tprog);
+  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
   if (rv) {
 #pragma unroll
     for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
@@ -355,7 +383,8 @@ __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
-                 int* __restrict__ prog, long long* __restrict__ stamps) {
+                 double* __restrict__ H, size_t hs, int* __restrict__ prog,
+                 int* __restrict__ err, long long limit, long long* __restrict__ stamps) {
   constexpr int WV = SymW<D>::v;
   constexpr int IW = SymI<D>::v;
   constexpr int NW = kSymT / 64;
@@ -367,6 +396,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
   double* ini = sini[threadIdx.x >> 6];
   double* out = sout[threadIdx.x >> 6];
   const bool repel_ok = REPEL_ONE || weight_ok(repel);
+  bool give_up = false;  // a hand-over wait timed out (err is set)
   for (;;) {
     int qi = 0;
     if (lane == 0) qi = atomicAdd(queue, 1);
@@ -386,7 +416,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __builtin_amdgcn_s_setprio(0);
     } else {
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
-                                              repel_ok, F, rec, ini, out, spin, t_first);
+                                              repel_ok, F, H, hs, err, limit, give_up, rec, ini,
+                                              out, spin, t_first);
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
@@ -510,7 +541,8 @@ template <int D, bool REPEL_ONE, bool STAMP>
 __device__ __forceinline__ void pair_unit(int lane, int A, int base, int s, int* tprog,
                                           const double* __restrict__ X,
                                           const double* __restrict__ DP, double repel,
-                                          bool repel_ok, double* __restrict__ F, double* rec,
+                                          bool repel_ok, double* __restrict__ F, int* err,
+                                          long long limit, bool& give_up, double* rec,
                                           double* ini, long long& spin, long long& t_first) {
   constexpr int IW = SymI<D>::v;
   const size_t cbase = (size_t)base + 64 * (size_t)A;
@@ -535,13 +567,10 @@ __device__ __forceinline__ void pair_unit(int lane, int A, int base, int s, int*
     const int qc = 64 * tt + lane;
     const bool cv = qc < ncols;  // tiles past the aggregate stage inert records
     if (A > 0 && tt < ntiles) {  // the units before have written column tile A + tt back
-      const long long t0 = STAMP ? rt_now() : 0;
-      while (__hip_atomic_load(tprog + tt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A)
-        __builtin_amdgcn_s_sleep(1);
+      const long long w = handover_wait<STAMP>(tprog + tt, A, err, limit, give_up);
       if (STAMP) {
-        const long long t1 = rt_now();
-        spin += t1 - t0;
-        if (tt == 0) t_first = t1;
+        spin += w;
+        if (tt == 0) t_first = rt_now();
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);  // as in sweep_unit
     }
@@ -605,10 +634,12 @@ __global__ void __launch_bounds__(64, 4)
 faml_sym_pair(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
               const int* __restrict__ pt_ip, const double* __restrict__ X,
               const double* __restrict__ DP, double repel, double* __restrict__ F,
-              int* __restrict__ prog, long long* __restrict__ stamps) {
+              int* __restrict__ prog, int* __restrict__ err, long long limit,
+              long long* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) double arena[pair_arena_doubles<D>()];
   const int lane = threadIdx.x;
   const bool repel_ok = REPEL_ONE || weight_ok(repel);
+  bool give_up = false;
   for (;;) {
     int qi = 0;
     if (lane == 0) qi = atomicAdd(queue, 1);
@@ -626,7 +657,8 @@ faml_sym_pair(int nunits, const int4* __restrict__ units, int* __restrict__ queu
       __builtin_amdgcn_s_setprio(0);
     } else {
       pair_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel, repel_ok, F,
-                                     arena, arena + (D + 1) * kPairRec, spin, t_first);
+                                     err, limit, give_up, arena, arena + (D + 1) * kPairRec, spin,
+                                     t_first);
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();

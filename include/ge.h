@@ -27,6 +27,7 @@ extern "C" {
 #define GE_ERR_HIP 1002     /* a HIP runtime call failed */
 #define GE_ERR_STATE 1003   /* object used in the wrong state */
 #define GE_ERR_NOMEM 1004   /* host allocation failed */
+#define GE_ERR_CAPACITY 1005 /* a device-side capacity limit (e.g. the partition's list pool) */
 
 #define GE_MODE_STRICT 0 /* bit-exact with the reference's serial op order */
 #define GE_MODE_FAST 1   /* re-associated / FMA / rsqrt; 1e-5 relative bar */

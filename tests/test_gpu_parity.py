@@ -279,6 +279,53 @@ def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("grp", ["0", "16", "32"])
+def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
+    """The coarsest level at its production size and horizon: an R-MAT LCC coarsened
+    twice by partition(A, 0.125) (n = 1067, integer weights, self-loops), seeded
+    random start, 100 000 iterations (src/embed.cpp:586) on the persistent
+    grid-barrier kernel, against the oracle's run of the same 1e5 iterations
+    (tests/golden/make_coarsest_1e5.py)."""
+    monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
+    if grp != "0":
+        monkeypatch.setenv("GE_GRP_G", grp)
+    g = golden("fa_coarsest_1e5")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    X = ctx.force_atlas(A, 3, iterations=int(g["iterations"]), seed=int(g["seed"]))
+    assert np.array_equal(X, g["x"])
+
+
+def test_fa_coarsest_level_shared_device(golden):
+    """Three contexts run the coarsest level on one GPU at once, as the ranks of a
+    one-GPU rehearsal do (every rank runs it as a replica): their persistent
+    grids cannot all be resident together, so a late one either waits for the
+    cooperative launch or times out at its barrier and reruns per iteration from
+    the restored start.  Every result is still the oracle's."""
+    import threading
+    g = golden("fa_coarsest_1e5")
+    A = (g["A_ip"], g["A_ix"], g["A_dx"])
+    its, seed = int(g["iterations"]), int(g["seed"])
+    ctxs = [ge.Context(0) for _ in range(3)]
+    out, errs = [None] * 3, []
+
+    def run(k):
+        try:
+            out[k] = ctxs[k].force_atlas(A, 3, iterations=its, seed=seed)
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for X in out:
+        assert np.array_equal(X, g["x"])
+
+
 def test_fa_nondefault_params(ctx, oracle):
     A = G.erdos_renyi(1500, 0.004, seed=5)
     X0 = G.random_coords(1500, 3, seed=2)

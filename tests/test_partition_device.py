@@ -23,6 +23,13 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+@pytest.fixture(autouse=True)
+def device_required(monkeypatch):
+    """A device-path failure of any kind (the list pool's capacity limit included)
+    fails the test instead of silently falling back to the host path."""
+    monkeypatch.setenv("GE_PARTITION_DEVICE_REQUIRE", "1")
+
+
 def same(hg, ho):
     assert len(hg) == len(ho)
     for a, b in zip(hg, ho):
