@@ -1048,9 +1048,14 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   // last arrival acquires its group's releases and releases them on to the grid
   // counter, and a waiter acquires with one fence after its relaxed poll.  Once per
   // iteration, so the L2 write-back / invalidate it implies costs little.
-  const int old = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef GE_BAR_ORDER
+#define GE_BAR_ORDER 2
+#endif
+  constexpr int kRel = GE_BAR_ORDER >= 1 ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
+  constexpr int kAR = GE_BAR_ORDER >= 1 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
+  const int old = __hip_atomic_fetch_add(gc, 1, kRel, __HIP_MEMORY_SCOPE_AGENT);
   if (old == members * (it + 1) - 1)  // the group's last arrival
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(cnt, 1, kAR, __HIP_MEMORY_SCOPE_AGENT);
   const int target = ngroups * (it + 1);
   const long long t0 = wall_clock64();
   while (coh_ldi(cnt) < target) {
@@ -1060,7 +1065,7 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (GE_BAR_ORDER >= 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return true;
 }
 
@@ -1407,6 +1412,21 @@ struct ge_fa_plan {
   bool profiling = false;
   std::vector<hipEvent_t> events;  // 3 per timed step
   size_t next_event = 0;
+  // Symmetric repulsion (ge_sym.hpp) for a whole large level in STRICT mode: the n
+  // vertices as one "aggregate" of T = ceil(n / 64) row tiles, every unordered pair
+  // evaluated once.  ctl = {queue, prog[T]}, zeroed before every launch.
+  bool sym = false;
+  int sym_units = 0, sym_blocks = 0;
+  long long sym_limit = 0;
+  ge::DevBuf<int4> units;
+  ge::DevBuf<int> ctl, seg;
+  ge::DevBuf<double> hand;
+  int* sym_err_h = nullptr;  // pinned, device-mapped: a timed-out hand-over wait
+  int* sym_err_d = nullptr;
+  ~ge_fa_plan() {
+    for (hipEvent_t e : events) (void)hipEventDestroy(e);
+    if (sym_err_h) (void)hipHostFree(sym_err_h);
+  }
 };
 
 namespace ge {
@@ -1442,6 +1462,37 @@ static void plan_init(ge_fa_plan* pl) {
                      pl->dx, pl->p.use_weights, pl->dp1.p);
   GE_HIP(hipGetLastError());
   GE_HIP(hipMemsetAsync(pl->fprev.p, 0, sizeof(double) * pl->fprev.n, s));
+  // Symmetric repulsion: STRICT, every row on this plan (a row shard keeps the
+  // ordered-pair kernel), and a level past the grouped / streamed kernels.
+  // GE_FA_SYM=0 keeps fa_repulse_strict (comparisons), GE_FA_SYM=1 forces it.
+  {
+    const char* e = std::getenv("GE_FA_SYM");
+    const bool force = e && *e == '1', off = e && *e == '0';
+    pl->sym = !off && pl->p.mode == GE_MODE_STRICT && pl->rb == 0 && pl->re == pl->n &&
+              (force || pl->n > stream_max());
+  }
+  if (pl->sym) {
+    const int T = (pl->n + 63) / 64;
+    std::vector<int4> h_units(T);
+    for (int A = 0; A < T; ++A) h_units[A] = make_int4(0, A, 0, 0);  // earliest start 2A
+    pl->sym_units = T;
+    pl->units.alloc(T);
+    pl->units.upload(h_units.data(), T, s);
+    pl->ctl.alloc(1 + 2 * T);  // queue, progress counters, (unused) band flags
+    const int h_seg[2] = {0, pl->n};
+    pl->seg.alloc(2);
+    pl->seg.upload(h_seg, 2, s);
+    pl->hand.alloc((size_t)pl->n * pl->dim);
+    pl->sym_blocks = pl->cus * sym_blocks_per_cu(pl->dim);
+    int dev = 0, khz = 0;
+    GE_HIP(hipGetDevice(&dev));
+    GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    pl->sym_limit = (long long)std::max(khz, 1000) * 5000;  // ~5 s per hand-over wait
+    GE_HIP(hipHostMalloc((void**)&pl->sym_err_h, sizeof(int), hipHostMallocMapped));
+    *pl->sym_err_h = 0;
+    GE_HIP(hipHostGetDevicePointer((void**)&pl->sym_err_d, pl->sym_err_h, 0));
+    GE_HIP(hipStreamSynchronize(s));
+  }
   // Gather copy, opt-in (GE_GATHER_COPY=1).  Measured without benefit: C2 attraction
   // 0.324 ms with it against 0.301 ms without, C5 31.8 against 30.3 ms; L2 misses
   // fell 14 % (FETCH 697 MB per C2 pass) but the long tail of low-degree
@@ -1482,6 +1533,17 @@ static void plan_gather_copy(ge_fa_plan* pl, const double* xc, hipStream_t s) {
                      pl->ginv.p, xc, pl->xg.p);
 }
 
+// A symmetric launch whose hand-over wait timed out (seen through the pinned
+// error word, without a synchronisation) fails the next step or the run's end.
+static void sym_check(ge_fa_plan* pl) {
+  if (pl->sym_err_h && __atomic_load_n(pl->sym_err_h, __ATOMIC_ACQUIRE)) {
+    *pl->sym_err_h = 0;
+    throw Error(GE_ERR_STATE, "forceAtlas: a symmetric sweep's hand-over wait timed out");
+  }
+}
+
+static void plan_free(ge_fa_plan* pl) { delete pl; }
+
 static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   hipStream_t s = pl->ctx->stream;
   hipEvent_t* ev = nullptr;
@@ -1505,8 +1567,17 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
       if (ev) GE_HIP(hipEventRecord(ev[1], s));
       return;
     }
-    launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
-                        pl->frep.p, pl->fpart.p, pl->cus);
+    if (pl->sym) {
+      sym_check(pl);
+      GE_HIP(hipMemsetAsync(pl->ctl.p, 0, sizeof(int) * pl->ctl.n, s));
+      sym_repulse_launch(D, pl->sym_blocks, s, pl->sym_units, pl->units.p, pl->ctl.p,
+                         pl->seg.p, xc, pl->dp1.p, pl->p.repel, pl->frep.p, pl->hand.p,
+                         (size_t)pl->n, pl->ctl.p + 1, pl->sym_units, pl->sym_err_d,
+                         pl->sym_limit);
+    } else {
+      launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
+                          pl->frep.p, pl->fpart.p, pl->cus);
+    }
     if (ev) GE_HIP(hipEventRecord(ev[1], s));
     plan_gather_copy<D>(pl, xc, s);
     launch_attract<D>(s, pl->rc, pl->rstreams, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
@@ -1739,6 +1810,7 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
   if (cur != d_x)
     GE_HIP(hipMemcpyAsync(d_x, cur, sizeof(double) * n * dim, hipMemcpyDeviceToDevice, s));
   GE_HIP(hipStreamSynchronize(s));
+  sym_check(&pl);
 }
 
 }  // namespace ge
@@ -1804,6 +1876,7 @@ int ge_fa_plan_kernel_ms(ge_fa_plan* pl, double* rep_ms, double* attr_ms, int* l
     GE_REQUIRE(pl && rep_ms && attr_ms && launches, "null argument");
     ge::DeviceGuard g(pl->ctx);
     GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+    ge::sym_check(pl);
     double a = 0.0, b = 0.0;
     int cnt = 0;
     for (size_t k = 0; k + 3 <= pl->next_event; k += 3) {
@@ -1821,11 +1894,7 @@ int ge_fa_plan_kernel_ms(ge_fa_plan* pl, double* rep_ms, double* attr_ms, int* l
 }
 
 int ge_fa_plan_destroy(ge_fa_plan* pl) {
-  return ge::guarded([&] {
-    if (!pl) return;
-    for (hipEvent_t e : pl->events) (void)hipEventDestroy(e);
-    delete pl;
-  });
+  return ge::guarded([&] { ge::plan_free(pl); });
 }
 
 }  // extern "C"

@@ -732,6 +732,7 @@ struct ge_faml_plan {
   ge::DevBuf<int> sym_err;  // set by a hand-over wait that timed out
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
+  int banded = 0;  // streamed aggregates run in bands (ge_sym.hpp)
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
   std::string stamp_path;
@@ -936,60 +937,111 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     pl->sym_blocks = cus * bpc;
     // a pair unit carries two row tiles: count its wave twice in the model
     const double waves = (double)pl->sym_blocks * (sym_threads / 64) * (pl->sym_pair ? 2 : 1);
-    std::vector<size_t> by_T(big.size());
-    std::iota(by_T.begin(), by_T.end(), 0);
-    std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
-    std::vector<char> rows_mode(big.size(), 0);
-    // Choose how many of the largest aggregates run as row blocks: the launch
-    // lasts about max(work / waves, the longest row block ~row_k T, the start of
-    // the sweeps + the longest sweep chain ~chain_k T) tile-times, where a sweep
-    // aggregate costs T^2 / 2 + T sweep-tiles and a row-block aggregate 0.8 T^2
-    // (every ordered pair; its waves run at raised priority).  Row blocks are first
-    // in the queue, so when they hold most of the waves the sweeps start late and
-    // run slower than modelled beside the raised row waves: mixes whose row blocks
-    // exceed half the waves are not taken (measured on per-rank shares of C4,
-    // N = 4: 20 of 24 aggregates as row blocks 70 ms per iteration, 7 of 25 (4 090
-    // row blocks) 58 ms, all 52 ms).
-    // Take the count that minimises it.
+    // Per streamed aggregate: plain sweeps (K = 1), K bands (ge_sym.hpp: pre row
+    // blocks, in-band sweeps, post row blocks), or whole row blocks (kRowsMode).
+    // The launch lasts about max(work / waves, the start of the sweeps + the longest
+    // chain) tile-times, where
+    //   sweeps:  work T^2 / 2 + T,               chain chain_k T
+    //   K bands: work sum_b (Tb^2 / 2 + Tb) + row_k sum_b Tb (T - Tb),
+    //            chain max_b (row_k b0 + chain_k Tb + row_k (T - b1))
+    //   rows:    work row_k T^2,                 chain row_k T
+    // (a row block evaluates every ordered pair at ~0.8 the step cost of a sweep; a
+    // sweep chain is ~2.5 T because each sweep starts ~2 tiles behind the one before).
+    // Row-block units (whole, pre) are first in the queue, so when they hold more than
+    // the waves the sweeps start late (start = their work / waves).  Greedy: while the
+    // longest chain sets the time, step its aggregate to the next option (more bands,
+    // then rows) if that lowers the prediction.  At N = 1 (C4) the launch is
+    // work-bound and nothing changes; the shares of a multi-GPU run are chain-bound.
+    constexpr int kRowsMode = 1 << 20;
     double chain_k = 2.5, row_k = 0.8;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
-    double best = 1e300;
-    size_t best_k = 0;
-    if (chain_k > 0.0 && any_big) {
-      double work = 0.0, row_work = 0.0, row_units = 0.0;
-      for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
-      for (size_t k = 0; k <= by_T.size(); ++k) {  // the k largest as row blocks
-        const double start = row_units > waves ? row_work / waves : 0.0;
-        const double sweep_chain = k < by_T.size() ? start + chain_k * T[by_T[k]] : 0.0;
-        const double row_path = k > 0 ? row_k * T[by_T[0]] : 0.0;
-        const double pred = std::max(work / waves, std::max(sweep_chain, row_path));
-        const bool mixed_late = 2.0 * row_units > waves && k < by_T.size();
-        if (!mixed_late && pred < best * 0.999) {
-          best = pred;
-          best_k = k;
-        }
-        if (k < by_T.size()) {
-          const double t = T[by_T[k]];
-          work += 0.8 * t * t - (0.5 * t * t + t);
-          row_work += 0.8 * t * t;
-          row_units += t;
+    int force_bands = 0;  // GE_FAML_SYM_BANDS=K: every streamed aggregate in K bands (tests)
+    if (const char* e = std::getenv("GE_FAML_SYM_BANDS")) force_bands = std::max(0, std::atoi(e));
+    auto band_lo = [](int Tb, int K, int i) { return (int)((long long)Tb * i / K); };
+    auto cost_of = [&](int Tb, int K, double& work, double& chain, double& rwork) {
+      const double t = Tb;
+      if (K == kRowsMode) {
+        work = rwork = row_k * t * t;
+        chain = row_k * t;
+        return;
+      }
+      work = rwork = chain = 0.0;
+      for (int i = 0; i < K; ++i) {
+        const double b0 = band_lo(Tb, K, i), b1 = band_lo(Tb, K, i + 1), tb = b1 - b0;
+        work += 0.5 * tb * tb + tb + row_k * tb * (t - tb);
+        rwork += row_k * tb * b0;  // the pre blocks (first in the queue)
+        chain = std::max(chain, row_k * b0 + chain_k * tb + row_k * (t - b1));
+      }
+    };
+    static const int kOptions[] = {1, 2, 3, 4, 6, 8, kRowsMode};
+    std::vector<int> opt(big.size(), 0);  // index into kOptions
+    auto mode_of = [&](size_t b) {
+      if (force_bands > 0) return std::min(force_bands, std::max(1, T[b] / 2));
+      return kOptions[opt[b]];
+    };
+    auto predict = [&](size_t* crit) {
+      double work = 0.0, rwork = 0.0, runits = 0.0, chain = 0.0;
+      size_t arg = 0;
+      std::vector<double> ch(big.size());
+      for (size_t b = 0; b < big.size(); ++b) {
+        double w, c, r;
+        const int K = mode_of(b);
+        cost_of(T[b], K, w, c, r);
+        work += w;
+        rwork += r;
+        if (K != 1) runits += K == kRowsMode ? T[b] : T[b] - band_lo(T[b], K, 1);
+        ch[b] = c;
+      }
+      const double start = runits > waves ? rwork / waves : 0.0;
+      for (size_t b = 0; b < big.size(); ++b) {
+        const double c = ch[b] + (mode_of(b) == kRowsMode ? 0.0 : start);
+        if (c > chain) {
+          chain = c;
+          arg = b;
         }
       }
-      for (size_t k = 0; k < best_k; ++k) rows_mode[by_T[k]] = 1;
-      if (std::getenv("GE_FAML_PLAN_DEBUG"))
-        std::fprintf(stderr,
-                     "faml plan: %zu streamed aggregates, T max %d, waves %.0f, work/waves %.1f "
-                     "(all sweeps), %zu as row blocks, predicted %.1f tile-times\n",
-                     big.size(), T[by_T[0]], waves,
-                     [&] {
-                       double w = 0.0;
-                       for (int t : T) w += 0.5 * t * (double)t + t;
-                       return w / waves;
-                     }(),
-                     best_k, best);
+      if (crit) *crit = arg;
+      return std::max(work / waves, chain);
+    };
+    double best = any_big ? predict(nullptr) : 0.0;
+    if (chain_k > 0.0 && any_big && force_bands == 0) {
+      const int nopt = sizeof(kOptions) / sizeof(kOptions[0]);
+      for (;;) {
+        size_t crit = 0;
+        predict(&crit);
+        // sweep pairs have no banded form; bands need 2 tiles each and 14-bit indices
+        int next = opt[crit] + 1;
+        while (next < nopt && kOptions[next] != kRowsMode &&
+               (pl->sym_pair || kOptions[next] > T[crit] / 2 || T[crit] > kUnitMaxTile))
+          ++next;
+        if (next >= nopt) break;
+        const int keep = opt[crit];
+        opt[crit] = next;
+        // equal counts as progress: aggregates of one size tie for the longest chain
+        // and the prediction falls only once every one of them has moved
+        const double p = predict(nullptr);
+        if (p <= best * (1.0 + 1e-12)) {
+          best = std::min(best, p);
+        } else {
+          opt[crit] = keep;
+          break;
+        }
+      }
     }
-    struct Unit { int a, A, pb, T, kind; double est; };
+    if (std::getenv("GE_FAML_PLAN_DEBUG") && any_big) {
+      int nb = 0, nr = 0;
+      for (size_t b = 0; b < big.size(); ++b) {
+        nb += mode_of(b) != 1 && mode_of(b) != kRowsMode;
+        nr += mode_of(b) == kRowsMode;
+      }
+      std::fprintf(stderr,
+                   "faml plan: %zu streamed aggregates, T max %d, waves %.0f, %d banded, %d as "
+                   "row blocks, predicted %.1f tile-times\n",
+                   big.size(), *std::max_element(T.begin(), T.end()), waves, nb, nr, best);
+    }
+    pl->banded = 0;
+    struct Unit { int a, A, pb, T, word; double est; };
     std::vector<Unit> us;
     int pb = 0;
     // Queue position of sweep A of an aggregate of T row tiles: 2A Tmax / T, i.e.
@@ -997,44 +1049,63 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // their last (chain-bound) sweeps together and the launch ends without a tail of
     // the largest aggregate's chain (C4: tail after the queue drained 8.7 -> 3.5 ms,
     // 148.1 -> 143.2 ms per launch).  GE_FAML_SYM_PROP=0: 2A, the sweep's earliest
-    // start (diagnostics; GE_FAML_SYM_EST scales the 2).
+    // start (diagnostics; GE_FAML_SYM_EST scales the 2).  In a band [b0, b1) the
+    // sweeps start after the pre blocks (row_k b0) and 2 (A - b0) into the band; a
+    // post block follows its sweep's b1 - A tiles.  Every unit comes after the units
+    // it waits on (pre before sweeps, sweep A - 1 before A, sweep A before post A).
     double est_k = 2.0;
     if (const char* e = std::getenv("GE_FAML_SYM_EST")) est_k = std::atof(e);
     const bool est_prop = !(std::getenv("GE_FAML_SYM_PROP") && *std::getenv("GE_FAML_SYM_PROP") == '0');
     const int Tmax = big.empty() ? 1 : *std::max_element(T.begin(), T.end());
-    auto est_of = [&](int A, int Tb) { return est_k * A * (est_prop ? (double)Tmax / Tb : 1.0); };
+    auto scale_of = [&](int Tb) { return est_prop ? (double)Tmax / Tb : 1.0; };
+    std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b) {
-      if (rows_mode[b]) continue;
+      const int K = mode_of(b);
+      if (K == kRowsMode) {
+        for (int A = 0; A < T[b]; ++A)
+          rows_units.push_back({big[b], A, 0, T[b], unit_word(kUnitRows, 0, 0), -1.0});
+        continue;
+      }
+      const double sc = scale_of(T[b]);
       if (pl->sym_pair) {  // row tiles (A, A + 1); a last odd tile with an inert second
-        for (int A = 0; A < T[b]; A += 2)
-          us.push_back({big[b], A, pb, T[b], 2, est_of(A, T[b])});
+        for (int A = 0; A < T[b]; A += 2) us.push_back({big[b], A, pb, T[b], 2, est_k * A * sc});
+      } else if (K == 1) {
+        for (int A = 0; A < T[b]; ++A)
+          us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, 0, 0), est_k * A * sc});
       } else {
-        for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], 0, est_of(A, T[b])});
+        ++pl->banded;
+        for (int i = 0; i < K; ++i) {
+          const int b0 = band_lo(T[b], K, i), b1 = band_lo(T[b], K, i + 1);
+          const bool last = i + 1 == K;
+          for (int A = b0; A < b1; ++A) {
+            if (b0 > 0)
+              rows_units.push_back({big[b], A, pb, T[b], unit_word(kUnitPre, b0, b1), -1.0});
+            const double e = (row_k * b0 + est_k * (A - b0)) * sc;
+            us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, b0, last ? 0 : b1), e});
+            if (!last)
+              us.push_back({big[b], A, pb, T[b], unit_word(kUnitPost, b0, b1),
+                            e + (b1 - A) * sc});
+          }
+        }
       }
       pb += T[b];
     }
-    std::vector<Unit> rows_units;
-    for (size_t b = 0; b < big.size(); ++b)
-      if (rows_mode[b])
-        for (int A = 0; A < T[b]; ++A) rows_units.push_back({big[b], A, 0, T[b], 1, 0.0});
     for (int a : split) {  // this rank's row tiles of the split aggregates: row blocks
       int t0, t1;
       tiles_of(a, rank, t0, t1);
       const int Ta = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
-      for (int A = t0; A < t1; ++A) rows_units.push_back({a, A, 0, Ta, 1, 0.0});
+      for (int A = t0; A < t1; ++A)
+        rows_units.push_back({a, A, 0, Ta, unit_word(kUnitRows, 0, 0), -1.0});
     }
-    // row blocks have no dependencies and each spans its aggregate's whole width:
-    // first in the queue (measured on per-rank shares of C4: N = 4 69 ms per
-    // iteration against 80 ms when spread among the sweeps, N = 2 unchanged)
-    for (size_t k = 0; k < rows_units.size(); ++k) {
-      rows_units[k].est = -1.0;
-      us.push_back(rows_units[k]);
-    }
+    // row blocks have no dependencies and each spans its aggregate's whole width (or
+    // the members before a band): first in the queue (measured on per-rank shares of
+    // C4: N = 4 69 ms per iteration against 80 ms when spread among the sweeps)
+    for (size_t k = 0; k < rows_units.size(); ++k) us.push_back(rows_units[k]);
     std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
       return x.est != y.est ? x.est < y.est : x.T > y.T;
     });
     std::vector<int4> h_units;
-    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.kind));
+    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.word));
     pl->nunits = (int)h_units.size();
     pl->ntiles = pb;
     pl->units.alloc(h_units.size());
@@ -1044,7 +1115,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       pl->h_units = h_units;
       pl->stamps.alloc(h_units.size() * kStampWords);
     }
-    pl->prog.alloc(std::max(pb, 1));
+    pl->prog.alloc(std::max(2 * pb, 1));  // progress counters, then the bands' rdone flags
     if (pb > 0) pl->hand.alloc((size_t)pl->n * dim);
     pl->sym_err.alloc(1);
     GE_HIP(hipMemsetAsync(pl->sym_err.p, 0, sizeof(int), st));
@@ -1188,7 +1259,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           GE_HIP(hipEventRecord(re[0], ss));
         }
         if (pl->sym) {
-          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
+          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * 2 * pl->ntiles, ss));
           double* H = pl->hand.p;
           const size_t hs = (size_t)pl->n;
           int* err = pl->sym_err.p;
@@ -1216,23 +1287,17 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim, pl->stamps.p);
+                               pl->ntiles, err, lim, pl->stamps.p);
 #endif
           } else if (!pl->stamp_path.empty()) {
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim, pl->stamps.p);
-          } else if (c.repel == 1.0) {
-            hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(pl->sym_blocks), dim3(kSymT), 0,
-                               ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p, err, lim,
-                               nullptr);
+                               pl->ntiles, err, lim, pl->stamps.p);
           } else {
-            hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(pl->sym_blocks), dim3(kSymT), 0,
-                               ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                               pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p, err, lim,
-                               nullptr);
+            sym_repulse_launch(D, pl->sym_blocks, ss, pl->nunits, pl->units.p, pl->queue.p + it,
+                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
+                               pl->ntiles, err, lim);
           }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
@@ -1309,6 +1374,37 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       std::fclose(f);
     }
   }
+}
+
+void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
+                        int* queue, const int* seg, const double* X, const double* DP,
+                        double repel, double* F, double* H, size_t hs, int* prog, int ptiles,
+                        int* err, long long limit) {
+  dispatch_dim(dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    if (repel == 1.0)
+      hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(blocks), dim3(kSymT), 0, s, nunits,
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, ptiles, err, limit,
+                         nullptr);
+    else
+      hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(blocks), dim3(kSymT), 0, s, nunits,
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, ptiles, err, limit,
+                         nullptr);
+  });
+  GE_HIP(hipGetLastError());
+}
+
+// three blocks (waves) per SIMD of the four that fit: fewer units in flight spin
+// less on hand-overs (C4 N = 1: 137.2 against 138.3 ms per launch; N = 8 shares
+// 30.0 against 32.7 ms; scripts/sym_timeline.py, profiles/r03/sym_timeline)
+int sym_blocks_per_cu(int dim) {
+  int occ = 1;
+  dispatch_dim(dim, [&](auto Dc) {
+    constexpr int D = decltype(Dc)::value;
+    GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
+  });
+  return std::min(std::max(occ, 1), 3);
 }
 
 static void faml_plan_free(ge_faml_plan* pl) {

@@ -157,6 +157,16 @@ void uniform_stream(unsigned seed, size_t count, double* out);
 void check_csr(int n, const int* ip, const int* ix, const double* dx);
 
 // Device entry points implemented in the .hip files, called by host drivers.
+// One launch of the symmetric all-pairs repulsion (ge_sym.hpp, faml_sym_repulse)
+// over `nunits` units {aggregate, row tile, progress offset, kind}; queue and
+// prog zeroed by the caller.  Defined in ge_faml.hip, shared with single-level
+// forceAtlas (ge_fa.hip).  sym_blocks_per_cu: the resident blocks it is sized for.
+void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
+                        int* queue, const int* seg, const double* X, const double* DP,
+                        double repel, double* F, double* H, size_t hs, int* prog, int ptiles,
+                        int* err, long long limit);
+int sym_blocks_per_cu(int dim);
+
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
                    const double* d_dx, int dim, double* d_x, int iterations,
                    const ge_fa_params& p);

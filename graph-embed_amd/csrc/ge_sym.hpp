@@ -193,8 +193,9 @@ __device__ __forceinline__ long long handover_wait(const int* flag, int A, int* 
     __builtin_amdgcn_s_sleep(1);
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A) break;
     if ((k & 255) == 0 &&
-        (rt_now() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (rt_now() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+      // system scope: err may be pinned host memory (single-level plans)
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       give_up = true;
       break;
     }
@@ -215,26 +216,30 @@ __device__ __forceinline__ void sym_steps_any(bool fast, int s0, int s1, int lan
                                          racc, flow);
 }
 
-// A row block of 64 rows against all s members in ascending order, every pair
-// evaluated for its row (the plain ordered-pair scheme: no dependencies).  Used
-// for aggregates whose sweep chain would outlast the rest of the launch.
+// A row block: the 64 rows of tile A against the members [c0, c1) in ascending
+// order, every pair evaluated for its row (the plain ordered-pair scheme: no
+// dependencies besides the start value).  acc starts at +0 or, with from_F, at the
+// rows' sums in F (agent-scope loads: another XCD's wave wrote them).  Used for
+// whole aggregates whose sweep chain would outlast the launch (c0 = 0, c1 = s) and
+// for the cross-band parts of banded aggregates (see faml_sym_repulse).
 template <int D, bool REPEL_ONE>
-__device__ __forceinline__ void rows_block(int lane, int base, int s, int A, const double* X,
-                                           const double* DP, double repel, bool repel_ok,
-                                           double* tile, double* F) {
+__device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int c0, int c1,
+                                           bool from_F, const double* X, const double* DP,
+                                           double repel, bool repel_ok, double* tile,
+                                           const double* F, double (&acc)[D]) {
   constexpr int WV = SymW<D>::v;
   const size_t rb = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
-  double xi[D], acc[D], di = 1.0;
+  double xi[D], di = 1.0;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     xi[k] = rv ? X[(rb + lane) * D + k] : 0.0;
-    acc[k] = 0.0;
+    acc[k] = (rv && from_F) ? agent_ld(F + (rb + lane) * D + k) : 0.0;
   }
   if (rv) di = DP[rb + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xi, di));
-  for (int j0 = 0; j0 < s; j0 += 64) {
-    const int cnt = min(64, s - j0);
+  for (int j0 = c0; j0 < c1; j0 += 64) {
+    const int cnt = min(64, c1 - j0);
     wave_lds_sync();  // the previous tile has been read by every lane
     bool ok = true;
     if (lane < cnt) {
@@ -254,11 +259,21 @@ __device__ __forceinline__ void rows_block(int lane, int base, int s, int A, con
                                   j0 + jj == 64 * A + lane, acc);
     }
   }
-  if (rv) {
+  wave_lds_sync();
+}
+
+// A whole row block (c0 = 0, c1 = s): the rows' final sums go to F.
+template <int D, bool REPEL_ONE>
+__device__ __forceinline__ void rows_block(int lane, int base, int s, int A, const double* X,
+                                           const double* DP, double repel, bool repel_ok,
+                                           double* tile, double* F) {
+  double acc[D];
+  rows_range<D, REPEL_ONE>(lane, base, s, A, 0, s, false, X, DP, repel, repel_ok, tile, F, acc);
+  if (64 * A + lane < s) {
+    const size_t rb = (size_t)base + 64 * (size_t)A;
 #pragma unroll
     for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = acc[k];
   }
-  wave_lds_sync();
 }
 
 // Per-unit timeline of one launch (STAMP builds only, GE_SYM_STAMPS): 8 words per
@@ -279,10 +294,12 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
                                            double* __restrict__ H, size_t hs, int* err,
                                            long long limit, bool& give_up, double* rec,
                                            double* ini, double* out, long long& spin,
-                                           long long& t_first) {
+                                           long long& t_first, int cend = 0,
+                                           int* rdone = nullptr) {
   constexpr int IW = SymI<D>::v;
   const size_t cbase = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
+  if (cend <= 0 || cend > s) cend = s;  // a band's sweeps stop at the band's end
   double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
 #pragma unroll
   for (int k = 0; k < D; ++k) {
@@ -292,7 +309,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   }
   if (rv) dr = DP[cbase + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
-  const int ncols = s - 64 * A;
+  const int ncols = cend - 64 * A;
   const int ntiles = (ncols + 63) >> 6;
   bool ok_prev = true;
   for (int tt = 0; tt < ntiles; ++tt) {
@@ -355,7 +372,18 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
                                        xr, dr, rv, repel, racc, flow);
   if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
-  if (rv) {
+  if (rdone) {
+    // a band before the last: the rows' sums continue in a post row block on
+    // another wave (another XCD): agent-scope stores, completed before the flag
+    if (rv) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) agent_st(F + (cbase + lane) * D + k, racc[k]);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) __hip_atomic_store(rdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (rv) {
 #pragma unroll
     for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
   }
@@ -373,9 +401,30 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
   w[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
 }
 
+// Banded aggregates.  A sweep chain is ~2.5 T tile-times however many CUs are
+// idle (each sweep starts ~2 tiles behind the one before), which bounds a share
+// of a multi-GPU run.  An aggregate cut into K bands of row tiles
+// [b0, b1) keeps the reference's per-row order as three parts per row:
+//   pre   (kind 3): the band's rows against the members before the band, as a row
+//         block; those sums are exactly the entering column sums of the band's
+//         first sweep, so they go to H and the band's tiles' progress counters
+//         are set to b0;
+//   sweeps (kind 0, band end b1): the band's rows and columns symmetric, each row
+//         continuing from its column sum at the diagonal as before;
+//   post  (kind 4): the band's rows against the members after the band, as a row
+//         block starting from the sweep's row sums (flag rdone[A]).
+// The chain of band b is ~0.8 b0 + 2.5 (b1 - b0) + 0.8 (T - b1) tile-times; the
+// cross-band pairs are evaluated twice (ordered), the in-band pairs once.
+constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3, kUnitPost = 4;
+__host__ __device__ inline int unit_word(int kind, int b0, int b1) {
+  return kind | (b0 << 4) | (b1 << 18);
+}
+constexpr int kUnitMaxTile = (1 << 14) - 1;  // band tile indices are 14-bit fields
+
 // units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
-// kind (0: symmetric sweep, 1: row block)} in queue order; prog zeroed before the
-// launch; queue = one counter.
+// unit_word(kind, band first tile, band end tile)} in queue order; prog (2 x
+// ptiles: progress counters, then the rdone flags) zeroed before the launch;
+// queue = one counter.  Every unit waits only on units before it in the queue.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
 // (diagnostics, wrong results): no sweep waits for its hand-overs.
 template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
@@ -383,7 +432,7 @@ __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
-                 double* __restrict__ H, size_t hs, int* __restrict__ prog,
+                 double* __restrict__ H, size_t hs, int* __restrict__ prog, int ptiles,
                  int* __restrict__ err, long long limit, long long* __restrict__ stamps) {
   constexpr int WV = SymW<D>::v;
   constexpr int IW = SymI<D>::v;
@@ -408,16 +457,49 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const int A = u.y;
     const int base = pt_ip[u.x];
     const int s = pt_ip[u.x + 1] - base;
-    if (u.w) {
+    const int kind = u.w & 15, b0 = (u.w >> 4) & kUnitMaxTile, b1 = (u.w >> 18) & kUnitMaxTile;
+    const size_t rb = (size_t)base + 64 * (size_t)A;
+    if (kind == kUnitRows) {
       // a row block spans its aggregate's whole width: the launch's critical path
       // when the aggregate is large, so its wave takes issue priority on the SIMD
       __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
+    } else if (kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
+      __builtin_amdgcn_s_setprio(3);
+      double acc[D];
+      rows_range<D, REPEL_ONE>(lane, base, s, A, 0, 64 * b0, false, X, DP, repel, repel_ok, rec,
+                               F, acc);
+      __builtin_amdgcn_s_setprio(0);
+      if (64 * A + lane < s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) agent_st(H + k * hs + rb + lane, acc[k]);
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_waitcnt(0);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane == 0)
+        __hip_atomic_store(prog + u.z + A, b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (kind == kUnitPost) {  // the band's rows after its sweeps
+      handover_wait<false>(prog + ptiles + u.z + A, 1, err, limit, give_up);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_setprio(3);
+      double acc[D];
+      rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b1, s, true, X, DP, repel, repel_ok, rec,
+                               F, acc);
+      __builtin_amdgcn_s_setprio(0);
+      if (64 * A + lane < s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = acc[k];
+      }
     } else {
+      // a sweep; in a band that is not the aggregate's last, stop at the band's end
+      // and hand the row sums to the post block
+      const bool banded = b1 > 0 && 64 * b1 < s;
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, ini,
-                                              out, spin, t_first);
+                                              out, spin, t_first, banded ? 64 * b1 : 0,
+                                              banded ? prog + ptiles + u.z + A : nullptr);
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();

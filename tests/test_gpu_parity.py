@@ -134,6 +134,7 @@ def test_fa_repulsion_row_slots(ctx, oracle, monkeypatch, R):
     """fa_repulse_strict with R row slots x 8/R partners in flight per lane
     (row shards of N GPUs pick small R), ragged tiles and slot counts."""
     monkeypatch.setenv("GE_STREAM_MAX", "0")  # the large-level kernels
+    monkeypatch.setenv("GE_FA_SYM", "0")  # the ordered-pair kernel (row shards use it)
     monkeypatch.setenv("GE_REP_R", R)
     A = G.rmat(9000, 60000, seed=3)
     n = len(A[0]) - 1
@@ -148,6 +149,7 @@ def test_fa_repulsion_full_row_slots(ctx, oracle, monkeypatch, R):
     row slot of a wave is filled (the branch-free path with the partner's
     record read once for all R rows), plus the ragged last chunk."""
     monkeypatch.setenv("GE_STREAM_MAX", "0")
+    monkeypatch.setenv("GE_FA_SYM", "0")  # the ordered-pair kernel (row shards use it)
     monkeypatch.setenv("GE_REP_R", R)
     monkeypatch.setenv("GE_REP_BLOCKS", "2")  # 4544 rows per block
     A = G.rmat(9000, 60000, seed=5)
@@ -155,6 +157,38 @@ def test_fa_repulsion_full_row_slots(ctx, oracle, monkeypatch, R):
     X0 = G.random_coords(n, 3, seed=9)
     want = oracle.force_atlas(A, 3, coords=X0, iterations=3)
     assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=3), want)
+
+
+@pytest.mark.parametrize("n,dim,repel", [(9000, 3, 1.0), (5000, 1, 1.0), (4097, 2, 1.0),
+                                          (3000, 4, 1.0), (6500, 3, 1.7), (64, 3, 1.0),
+                                          (65, 2, 1.0), (200, 3, 1e21)])
+def test_fa_symmetric_repulsion(ctx, oracle, monkeypatch, n, dim, repel):
+    """Single-level forceAtlas with the symmetric sweeps (ge_sym.hpp): the level as
+    one aggregate of ceil(n / 64) row tiles, each unordered pair evaluated once,
+    column sums handed from sweep to sweep; ragged last tile, one and two tiles,
+    every dimension, repel != 1 and a repel large enough (1e21) to leave the
+    shared-reciprocal domain (the `/` forms)."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")
+    monkeypatch.setenv("GE_FA_SYM", "1")
+    A = G.rmat(n, 6 * n, seed=n + dim)
+    m = len(A[0]) - 1
+    X0 = G.random_coords(m, dim, seed=dim)
+    want = oracle.force_atlas(A, dim, coords=X0, iterations=3, repel=repel)
+    assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=3, repel=repel), want)
+
+
+def test_fa_symmetric_repulsion_domain_and_ties(ctx, oracle, monkeypatch):
+    """Symmetric sweeps with a coordinate outside the exact-division domain (its
+    tiles take the `/` forms), coincident points (distance clamped to eps) and
+    isolated vertices, over enough iterations to replay a captured graph."""
+    monkeypatch.setenv("GE_STREAM_MAX", "0")
+    monkeypatch.setenv("GE_FA_SYM", "1")
+    A = G.rmat(3000, 12000, seed=44)
+    X0 = G.random_coords(3000, 3, seed=8)
+    X0[1500, 1] = 1e-70
+    X0[10] = X0[11]
+    want = oracle.force_atlas(A, 3, coords=X0, iterations=130)
+    assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=130), want)
 
 
 @pytest.mark.parametrize("hook", [("GE_SMALL_GENERAL_ONLY", "1"), ("GE_SMALL_HANDOVER", "37"),
@@ -512,6 +546,30 @@ def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
     rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
     want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
     got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("bands,dim,repel", [
+    ("2", 3, 1.0), ("3", 3, 1.0), ("4", 3, 1.5), ("8", 3, 1.0), ("2", 3, 2.0 ** 70),
+    ("3", 2, 1.0), ("4", 4, 0.75), ("2", 1, 1.0)])
+def test_faml_symmetric_bands(ctx, oracle, monkeypatch, bands, dim, repel):
+    """Banded aggregates (ge_sym.hpp): each streamed aggregate cut into K bands of
+    row tiles -- pre row blocks (the band's rows against the members before it,
+    handed to the band's first sweep as entering column sums), in-band sweeps, post
+    row blocks continuing from the sweeps' row sums -- keep every row's order of
+    additions; K = 2..8 (capped at half the tiles), the `/` path, every dimension."""
+    monkeypatch.setenv("GE_FAML_SYM", "1")
+    monkeypatch.setenv("GE_FAML_SYM_BANDS", bands)
+    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=13), [(3, 2000), (70, 3000)], seed=dim)
+    PT = _block_partition(n, sizes, seed=6)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m + 1)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=23, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=23, repel=repel)
     assert np.array_equal(got, want)
 
 
