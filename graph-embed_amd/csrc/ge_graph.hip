@@ -18,13 +18,13 @@
 //   (ascending original id), which keeps every row's columns ascending.
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdint>
 #include <vector>
 
 #include "ge_internal.hpp"
+#include "ge_prim.hpp"
 
 namespace ge {
 namespace {
@@ -164,7 +164,7 @@ __global__ void lcc_copy_kernel(int n, const int* __restrict__ ip, const int* __
   }
 }
 
-// Library calls (hipcub sort / scan) on at most this many items each: the C5
+// Library calls (rocPRIM sort / scan) on at most this many items each: the C5
 // generator has 1.6e9 directed draws, which is past what one call is trusted with.
 constexpr long long kChunk = 1ll << 28;
 
@@ -184,10 +184,7 @@ __global__ void add_carry_kernel(long long len, int* __restrict__ out,
 template <class T>
 void exclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
   if (count <= kChunk) {
-    size_t tmp = 0;
-    GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)count, st));
-    DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
-    GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, in, out, (int)count, st));
+    prim_exclusive_sum(st, in, out, (size_t)count);
     return;
   }
   // chunks of kChunk, each shifted by the running total of the ones before
@@ -195,13 +192,9 @@ void exclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
   const int nc = (int)((count + kChunk - 1) / kChunk);
   DevBuf<int> carry(nc + 1);
   GE_HIP(hipMemsetAsync(carry.p, 0, sizeof(int) * (nc + 1), st));
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)kChunk, st));
-  DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
   for (int c = 0; c < nc; ++c) {
     const long long c0 = c * kChunk, len = std::min(kChunk, count - c0);
-    size_t t2 = tmp;
-    GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, t2, in + c0, out + c0, (int)len, st));
+    prim_exclusive_sum(st, in + c0, out + c0, (size_t)len);
     hipLaunchKernelGGL(chunk_total_kernel, dim3(1), dim3(1), 0, st,
                        (const int*)(out + c0 + len - 1), (const int*)(in + c0 + len - 1), carry.p, c);
     hipLaunchKernelGGL(add_carry_kernel, dim3(grid_for(len)), dim3(256), 0, st, len,
@@ -258,11 +251,10 @@ void rmat_device(ge_ctx* ctx, int n, long long draws, u64 seed, DCsr& out) {
                        (long long)n, splitmix64_host(seed), k.p);
   GE_HIP(hipGetLastError());
   if (L <= kChunk) {
-    size_t tmp = 0;
-    GE_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, k.p, k2.p, (int)L, 0, 64, st));
-    DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
+    const size_t tmp = prim_sort_keys_bytes(st, k.p, k2.p, (size_t)L, 64);
+    DevBuf<unsigned char> scratch(tmp);
     // all 64 bits: the kNoKey sentinel sorts last
-    GE_HIP(hipcub::DeviceRadixSort::SortKeys(scratch.p, tmp, k.p, k2.p, (int)L, 0, 64, st));
+    prim_sort_keys(st, scratch.p, tmp, k.p, k2.p, (size_t)L, 64);
   } else {
     // Large inputs: cut the valid keys into row ranges of at most kChunk keys
     // (row = key / n, so ranges of rows are ranges of keys), scatter each into its
@@ -297,15 +289,12 @@ void rmat_device(ge_ctx* ctx, int n, long long draws, u64 seed, DCsr& out) {
     hipLaunchKernelGGL(scatter_keys_kernel, dim3(grid_for(L)), dim3(256), 0, st, L, (long long)n,
                        nb, d_bound.p, d_boff.p, d_fill.p, k.p, k2.p);
     GE_HIP(hipGetLastError());
-    size_t tmp = 0;
-    GE_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, k2.p, k.p, (int)kChunk, 0, 64, st));
-    DevBuf<unsigned char> scratch(std::max<size_t>(tmp, 1));
+    const size_t tmp = prim_sort_keys_bytes(st, k2.p, k.p, (size_t)kChunk, 64);
+    DevBuf<unsigned char> scratch(tmp);
     for (int b = 0; b < nb; ++b) {
       const long long b0 = boff[b], b1 = b + 1 < nb ? boff[b + 1] : tot;
-      size_t t2 = tmp;
       if (b1 > b0)
-        GE_HIP(hipcub::DeviceRadixSort::SortKeys(scratch.p, t2, k2.p + b0, k.p + b0, (int)(b1 - b0),
-                                                 0, 64, st));
+        prim_sort_keys(st, scratch.p, tmp, k2.p + b0, k.p + b0, (size_t)(b1 - b0), 64);
     }
     std::swap(k.p, k2.p);  // the sorted keys are in k2 from here on, as in the small path
     L = tot;

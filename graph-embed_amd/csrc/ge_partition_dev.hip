@@ -35,7 +35,6 @@
 // reference's map size, which orients each merge, :1737-1743).
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -50,6 +49,7 @@
 #include <vector>
 
 #include "ge_internal.hpp"
+#include "ge_prim.hpp"
 
 namespace ge {
 namespace {
@@ -1744,10 +1744,7 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                            capbuf.p);
         GE_HIP(hipMemsetAsync(capbuf.p + n, 0, sizeof(long long), st));
         DevBuf<long long> noff(n + 1);
-        size_t tmp = 0;
-        GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, capbuf.p, noff.p, n + 1, st));
-        DevBuf<unsigned char> scratch(tmp);
-        GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, capbuf.p, noff.p, n + 1, st));
+        prim_exclusive_sum(st, capbuf.p, noff.p, (size_t)n + 1);
         int* nkey = (d.akey == key_a.p) ? key_b.p : key_a.p;
         double* nwt = (d.aw == w_a.p) ? w_b.p : w_a.p;
         hipLaunchKernelGGL(compact_copy_kernel, dim3(2048), dim3(256), 0, st, d, noff.p, nkey, nwt);

@@ -30,13 +30,13 @@
 // share in ge_ptap_dist); agg(j) always uses the whole P_T.
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
 
 #include "ge_internal.hpp"
+#include "ge_prim.hpp"
 
 namespace ge {
 namespace {
@@ -184,29 +184,19 @@ __global__ void run_sum_kernel(long long L, const int* __restrict__ nruns_p, int
 
 template <class K, class V>
 void sort_pairs(hipStream_t st, K*& k, K*& k2, V*& v, V*& v2, long long L, int end_bit) {
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k, k2, v, v2, (int)L, 0, end_bit, st));
-  DevBuf<unsigned char> scratch(tmp);
-  GE_HIP(hipcub::DeviceRadixSort::SortPairs(scratch.p, tmp, k, k2, v, v2, (int)L, 0, end_bit,
-                                            st));
+  prim_sort_pairs(st, k, k2, v, v2, (size_t)L, end_bit);
   std::swap(k, k2);
   std::swap(v, v2);
 }
 
 template <class T>
 void exclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (int)count, st));
-  DevBuf<unsigned char> scratch(tmp);
-  GE_HIP(hipcub::DeviceScan::ExclusiveSum(scratch.p, tmp, in, out, (int)count, st));
+  prim_exclusive_sum(st, in, out, (size_t)count);
 }
 
 template <class T>
 void inclusive_scan(hipStream_t st, const T* in, T* out, long long count) {
-  size_t tmp = 0;
-  GE_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tmp, in, out, (int)count, st));
-  DevBuf<unsigned char> scratch(tmp);
-  GE_HIP(hipcub::DeviceScan::InclusiveSum(scratch.p, tmp, in, out, (int)count, st));
+  prim_inclusive_sum(st, in, out, (size_t)count);
 }
 
 }  // namespace
