@@ -460,6 +460,9 @@ def run_multilevel(args, rank, world, local, dev):
                                 "rows": att_rows, "entries": att_entries,
                                 "avg_launch_ms": att_ms, "launches": att_passes},
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
+        # this rank's streamed aggregates: plain symmetric sweeps / bands (a shorter
+        # dependency chain) / whole row blocks
+        "sym_schedule": pk.schedule(),
         "setup_seconds": {"graph_device": t_gen, "partition_device": t_part,
                           "partition_host": t_part_host, "ptap_device": t_ptap,
                           "plan_build": plan_seconds.get(args.steps),

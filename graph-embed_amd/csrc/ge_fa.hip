@@ -833,6 +833,16 @@ __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
   return ok;
 }
 
+// Persistent small-level barrier ordering (tuning switch, scripts/build_variant.sh):
+// 0 relaxed arrival + agent-scope staging loads; 1 release arrival; 2 release + an
+// acquire fence after the poll; 3 acquire fence only and plain (L2-cached) staging
+// loads; 4 release + acquire and plain staging loads.  The coordinates are always
+// stored with agent-scope stores.
+#ifndef GE_BAR_ORDER
+#define GE_BAR_ORDER 2
+#endif
+constexpr bool kBarCohStage = GE_BAR_ORDER < 3;
+
 constexpr int kGrpT = 256;
 constexpr int grouped_cap(int D) { return (D + 1 <= 4) ? 3072 : 1536; }  // <= 96 KiB of records
 inline size_t grouped_lds_bytes(int n, int D) {
@@ -919,7 +929,8 @@ __device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re
   const int i = rb + blk * (kGrpT / G) + tid / G;
   const bool active = i < re;
   const bool ok =
-      stage_records<D, kGrpT, 4, COH>(X, dp1, 0, n, rec) && (REPEL_ONE || weight_ok(c.repel));
+      stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
+      (REPEL_ONE || weight_ok(c.repel));
   double xi[D], acc[D], fprev[D];
   const int e0 = active ? ip[i] : 0;
   const int e1 = active ? ip[i + 1] : 0;
@@ -993,6 +1004,149 @@ __device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re
 }
 
 
+// Packed rows (the coarsest level's persistent kernel, 4 rows per block as with 64
+// lanes per row).  With one wave per row, each chunk of 64 partners costs the
+// wave its 64 terms AND 64 ordered adds (one full-wave instruction each for 3
+// active lanes), ~13 ns per partner at n ~ 1000.  Here wave 0 only adds: lane
+// r * D + k carries row r's dimension k (12 lanes for 4 rows in 3-D), one dependent
+// add per term, while waves 1-3 evaluate the next chunk of kPackU x 48 partners
+// per row into the other half of a double buffer.  The per-row order of additions
+// is the reference's (partners ascending, then the CSR row in stored order), so
+// the bits are those of grouped_iteration.  In-domain blocks only: a block whose
+// records leave the exact-division domain runs grouped_iteration<G = 64> (the same
+// rows) instead.
+constexpr int kPackR = kGrpT / 64;                     // rows per block
+constexpr int kPackU = 2;                               // terms per producer lane per chunk
+constexpr int kPackC = (kGrpT - 64) / kPackR * kPackU;  // partners per row per chunk (96)
+inline size_t packed_lds_bytes(int n, int D) {
+  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kPackR * D * kPackC);
+}
+
+template <int D, bool REPEL_ONE, bool LINEAR, bool COH>
+__device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
+                                                 const int* __restrict__ ip,
+                                                 const int* __restrict__ ix,
+                                                 const double* __restrict__ dx,
+                                                 const double* __restrict__ X,
+                                                 const double* __restrict__ dp1, const FaConst& c,
+                                                 double* __restrict__ Fprev,
+                                                 double* __restrict__ Xnext, double* smem) {
+  static_assert(kPackR * D <= 64, "one adder lane per (row, dimension)");
+  static_assert(kPackC % 16 == 0, "group_chain reads batches of 16");
+  constexpr int W = Rec<D>::W;
+  constexpr int PL = kGrpT - 64;               // producer lanes
+  constexpr int CL = PL / kPackR;              // producer lanes per row
+  constexpr int BUF = kPackR * D * kPackC;     // one half of the term buffer
+  __shared__ int s_e[kPackR][2];
+  double* rec = smem;
+  double* tb = smem + (size_t)n * W;
+  const int tid = threadIdx.x;
+  const int r0 = rb + blk * kPackR;
+  const bool ok =
+      stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
+      (REPEL_ONE || weight_ok(c.repel));
+  if (tid < kPackR) {
+    const int i = r0 + tid;
+    s_e[tid][0] = i < re ? ip[i] : 0;
+    s_e[tid][1] = i < re ? ip[i + 1] : 0;
+  }
+  if (!__syncthreads_and(ok)) {  // block-uniform: the general bodies, same rows
+    grouped_iteration<D, 64, REPEL_ONE, LINEAR, COH>(blk, n, rb, re, ip, ix, dx, X, dp1, c, Fprev,
+                                                     Xnext, smem);
+    return;
+  }
+  // producer lane: row pr, chunk slots pj + CL * u
+  const bool prod = tid >= 64;
+  const int p = tid - 64, pr = prod ? p / CL : 0, pj = prod ? p % CL : 0;
+  const int ip_row = r0 + pr;
+  const bool pact = prod && ip_row < re;
+  double xp[D], dp = 1.0;
+#pragma unroll
+  for (int k = 0; k < D; ++k) xp[k] = pact ? rec[ip_row * W + k] : 0.0;
+  if (pact) dp = rec[ip_row * W + D];
+  auto rep_chunk = [&](int ch, double* dst) {  // terms of partners ch * C + slot
+    double t[kPackU][D];
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int j = ch * kPackC + pj + CL * u;
+      const int jj = min(j, n - 1);
+      rep_term<D, true, REPEL_ONE>(xp, &rec[jj * W], dp, rec[jj * W + D], c.repel, t[u]);
+      if (j >= n || !pact)
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u)
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackC + pj + CL * u] = t[u][k];
+  };
+  const int pe0 = s_e[pr][0], pe1 = s_e[pr][1];
+  auto att_chunk = [&](int ch, double* dst) {  // CSR entries e0 + ch * C + slot
+    double t[kPackU][D];
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u) {
+      const int q = ch * kPackC + pj + CL * u;
+      const int ee = min(pe0 + q, pe1 - 1);
+#pragma unroll
+      for (int k = 0; k < D; ++k) t[u][k] = 0.0;
+      if (pact && pe0 + q < pe1)
+        attr_edge<D, true, LINEAR>(xp, &rec[ix[ee] * W], c.use_weights ? dx[ee] : 1.0, dp, c,
+                                   t[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kPackU; ++u)
+#pragma unroll
+      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackC + pj + CL * u] = t[u][k];
+  };
+  // adder lane: row ar, dimension ak
+  const int ar = tid / D, ak = tid - ar * D;
+  const bool adder = tid < kPackR * D;
+  double a = 0.0;
+  const int nrep = (n + kPackC - 1) / kPackC;
+  int maxdeg = 0;
+#pragma unroll
+  for (int r = 0; r < kPackR; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
+  const int natt = (maxdeg + kPackC - 1) / kPackC;
+  const int ntot = nrep + natt;  // the repulsion chunks, then the attraction chunks
+  const int adeg = adder ? s_e[ar][1] - s_e[ar][0] : 0;
+  if (prod && ntot > 0) {
+    if (nrep > 0) rep_chunk(0, tb);
+    else att_chunk(0, tb);
+  }
+  __syncthreads();
+  for (int ch = 0; ch < ntot; ++ch) {
+    const double* cur = tb + (ch & 1) * BUF;
+    if (tid < 64) {
+      if (adder) {
+        const int cnt = ch < nrep ? min(kPackC, n - ch * kPackC)
+                                  : min(kPackC, max(0, adeg - (ch - nrep) * kPackC));
+        if (cnt > 0) a = group_chain<kPackC>(a, cur + (ar * D + ak) * kPackC, cnt);
+      }
+    } else if (ch + 1 < ntot) {
+      double* nxt = tb + ((ch + 1) & 1) * BUF;
+      if (ch + 1 < nrep) rep_chunk(ch + 1, nxt);
+      else att_chunk(ch + 1 - nrep, nxt);
+    }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    // the row's leader lane (r * D) gathers its dimensions, then gravity / update
+    double acc[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) acc[k] = __shfl(a, (tid / D) * D + k);
+    const int i = r0 + ar;
+    if (adder && ak == 0 && i < re) {
+      double xi[D], fprev[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        xi[k] = rec[i * W + k];
+        fprev[k] = Fprev[(size_t)(i - rb) * D + k];
+      }
+      finish_row<D, COH>(i, i - rb, xi, acc, fprev, rec[i * W + D], c, Fprev, Xnext, true);
+    }
+  }
+}
+
 template <int D, int G, bool REPEL_ONE, bool LINEAR>
 __global__ void __launch_bounds__(kGrpT)
 fa_grouped_step(int n, int rb, int re, const int* __restrict__ ip, const int* __restrict__ ix,
@@ -1048,11 +1202,9 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   // last arrival acquires its group's releases and releases them on to the grid
   // counter, and a waiter acquires with one fence after its relaxed poll.  Once per
   // iteration, so the L2 write-back / invalidate it implies costs little.
-#ifndef GE_BAR_ORDER
-#define GE_BAR_ORDER 2
-#endif
-  constexpr int kRel = GE_BAR_ORDER >= 1 ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
-  constexpr int kAR = GE_BAR_ORDER >= 1 ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
+  constexpr bool rel = GE_BAR_ORDER == 1 || GE_BAR_ORDER == 2 || GE_BAR_ORDER == 4;
+  constexpr int kRel = rel ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
+  constexpr int kAR = rel ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
   const int old = __hip_atomic_fetch_add(gc, 1, kRel, __HIP_MEMORY_SCOPE_AGENT);
   if (old == members * (it + 1) - 1)  // the group's last arrival
     __hip_atomic_fetch_add(cnt, 1, kAR, __HIP_MEMORY_SCOPE_AGENT);
@@ -1069,7 +1221,7 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   return true;
 }
 
-template <int D, int G, bool REPEL_ONE, bool LINEAR>
+template <int D, int G, bool REPEL_ONE, bool LINEAR, bool PACKED = false>
 __global__ void __launch_bounds__(kGrpT)
 fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__ ix,
                       const double* __restrict__ dx, double* __restrict__ Xa,
@@ -1081,8 +1233,12 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
   for (int it = 0; it < iterations; ++it) {
     const double* X = (it & 1) ? Xb : Xa;
     double* Xn = (it & 1) ? Xa : Xb;
-    grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
-                                                     Fprev, Xn, smem);
+    if constexpr (PACKED)
+      packed_iteration<D, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
+                                                   Fprev, Xn, smem);
+    else
+      grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1,
+                                                       c, Fprev, Xn, smem);
     if (it + 1 == iterations) break;
     // this thread's coordinate stores have completed before the block arrives;
     // the signal fences keep the compiler from moving memory accesses across
@@ -1484,6 +1640,8 @@ static void plan_init(ge_fa_plan* pl) {
     pl->seg.upload(h_seg, 2, s);
     pl->hand.alloc((size_t)pl->n * pl->dim);
     pl->sym_blocks = pl->cus * sym_blocks_per_cu(pl->dim);
+    if (const char* e = std::getenv("GE_FA_SYM_BLOCKS"))  // tuning: blocks per CU
+      pl->sym_blocks = pl->cus * std::max(1, std::min(4, std::atoi(e)));
     int dev = 0, khz = 0;
     GE_HIP(hipGetDevice(&dev));
     GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
@@ -1618,10 +1776,9 @@ static void plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, d
 }
 
 // All iterations of a small level (n <= grouped_cap, every row) in one launch of
-// fa_grouped_persistent.  The grid must fit the device at half its block
-// occupancy: the lanes per row halve from grouped_lanes(n) until it does.  The
-// launch is cooperative, so the runtime either makes the whole grid resident or
-// refuses it.  Other work on the device (another rank's persistent kernel on the
+// fa_grouped_persistent.  The grid must fit the device at its block occupancy:
+// the lanes per row halve from grouped_lanes(n) until it does.  The launch is
+// cooperative, so the runtime either makes the whole grid resident or refuses it.  Other work on the device (another rank's persistent kernel on the
 // same GPU, another process) can still delay blocks past the barrier's ~2 s
 // bound: then the start state (coordinates, previous forces) is restored and the
 // caller runs the per-iteration path from it.  Returns false (nothing computed)
@@ -1634,7 +1791,8 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
   const int n = pl->n;
   if (n > grouped_cap(D) || pl->rb != 0 || pl->re != n) return false;
   hipStream_t s = pl->ctx->stream;
-  const size_t lds = grouped_lds_bytes(n, D);
+  // 64 lanes per row: the packed rows (packed_iteration) unless GE_FA_PACKED=0
+  const bool packed_on = !(std::getenv("GE_FA_PACKED") && *std::getenv("GE_FA_PACKED") == '0');
   bool launched = false, fits = false, refused = false;
   DevBuf<int> bar;
   // the start state, restored when the barrier times out
@@ -1646,12 +1804,17 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
     const int nb = (n + kGrpT / GC - 1) / (kGrpT / GC);
     auto one = [&](auto RO, auto LI) {
       constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
-      const void* fn = reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>);
+      const bool pk = GC == 64 && packed_on;
+      const size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D))
+                            : grouped_lds_bytes(n, D);
+      const void* fn =
+          pk ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN, GC == 64>)
+             : reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>);
       if (lds > 65536)
         GE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       int occ = 0;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kGrpT, lds));
-      if ((long long)nb * 2 > (long long)occ * pl->cus) return;
+      if ((long long)nb > (long long)occ * pl->cus) return;  // the whole grid resident
       fits = true;
       int dev = 0, khz = 0;
       GE_HIP(hipGetDevice(&dev));

@@ -732,7 +732,7 @@ struct ge_faml_plan {
   ge::DevBuf<int> sym_err;  // set by a hand-over wait that timed out
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
-  int banded = 0;  // streamed aggregates run in bands (ge_sym.hpp)
+  int banded = 0, rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
   std::string stamp_path;
@@ -1040,7 +1040,12 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
                    "row blocks, predicted %.1f tile-times\n",
                    big.size(), *std::max_element(T.begin(), T.end()), waves, nb, nr, best);
     }
-    pl->banded = 0;
+    pl->banded = pl->rows_mode = pl->swept = 0;
+    for (size_t b = 0; b < big.size(); ++b) {
+      const int K = mode_of(b);
+      if (K == kRowsMode) ++pl->rows_mode;
+      else if (K == 1 || pl->sym_pair) ++pl->swept;
+    }
     struct Unit { int a, A, pb, T, word; double est; };
     std::vector<Unit> us;
     int pb = 0;
@@ -1643,6 +1648,17 @@ int ge_faml_plan_rows_ms(ge_faml_plan* pl, double* ms, int* passes, long long* r
     }
     *ms = cnt ? t / cnt : 0.0;
     *passes = cnt;
+  });
+}
+
+int ge_faml_plan_schedule(ge_faml_plan* pl, int* sweeps, int* banded, int* row_blocks,
+                          int* units) {
+  return ge::guarded([&] {
+    GE_REQUIRE(pl && sweeps && banded && row_blocks && units, "null argument");
+    *sweeps = pl->swept;
+    *banded = pl->banded;
+    *row_blocks = pl->rows_mode;
+    *units = pl->nunits;
   });
 }
 

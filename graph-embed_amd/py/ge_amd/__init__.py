@@ -113,6 +113,7 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.c_double), _ip]),
     "ge_faml_plan_repulse_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _ip,
                                                ctypes.POINTER(ctypes.c_double)]),
+    "ge_faml_plan_schedule": (ctypes.c_int, [_vp, _ip, _ip, _ip, _ip]),
     "ge_faml_plan_rows_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), _ip,
                                             ctypes.POINTER(ctypes.c_longlong),
                                             ctypes.POINTER(ctypes.c_longlong)]),
@@ -584,6 +585,13 @@ class FamlPlan:
         _check(lib().ge_faml_plan_rows_ms(self.h, ctypes.byref(a), ctypes.byref(c),
                                           ctypes.byref(r), ctypes.byref(e)))
         return a.value, c.value, r.value, e.value
+
+    def schedule(self):
+        """{sweeps, banded, row_blocks, units}: how the streamed aggregates' repulsion
+        is scheduled (ge_faml_plan_schedule)."""
+        v = [ctypes.c_int() for _ in range(4)]
+        _check(lib().ge_faml_plan_schedule(self.h, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("sweeps", "banded", "row_blocks", "units"), (x.value for x in v)))
 
     def close(self):
         if self.h:

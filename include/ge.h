@@ -157,6 +157,12 @@ int ge_faml_plan_repulse_ms(ge_faml_plan* plan, double* ms_per_launch, int* laun
  * iteration), the passes profiled, and the rows and CSR entries one pass reads. */
 int ge_faml_plan_rows_ms(ge_faml_plan* plan, double* ms_per_pass, int* passes,
                          long long* rows, long long* entries);
+/* The plan's schedule of the streamed aggregates' repulsion: how many run as
+ * plain symmetric sweeps, in bands (pre row blocks / in-band sweeps / post row
+ * blocks: a shorter dependency chain), as whole row blocks, and the units of
+ * one launch.  Diagnostics; the results do not depend on it. */
+int ge_faml_plan_schedule(ge_faml_plan* plan, int* sweeps, int* banded, int* row_blocks,
+                          int* units);
 int ge_faml_plan_destroy(ge_faml_plan* plan);
 
 /* ---- coarsening hierarchy ----

@@ -20,12 +20,15 @@ ctx = ge.Context()
 X0 = G.random_coords(n, 3, seed=1)
 ctx.force_atlas(A, 3, coords=X0, iterations=200)  # warm-up (module load, allocations)
 res = {}
-for mode in ("persistent", "graph"):
+for mode in ("persistent", "persistent-nopack", "graph"):
+    if mode == "persistent-nopack":  # 64 lanes per row: one wave per row, not packed
+        os.environ["GE_FA_PACKED"] = "0"
     if mode == "graph":
+        os.environ.pop("GE_FA_PACKED", None)
         os.environ["GE_NO_PERSIST"] = "1"
     t = time.perf_counter()
     res[mode] = ctx.force_atlas(A, 3, coords=X0, iterations=its)
     dt = time.perf_counter() - t
     print(f"{mode}: n={n} nnz={len(A[1])} iterations={its} {dt:.3f} s "
           f"({1e6 * dt / its:.2f} us/iteration)", flush=True)
-print("bit-identical:", bool(np.array_equal(res["persistent"], res["graph"])))
+print("bit-identical:", all(np.array_equal(res["persistent"], r) for r in res.values()))

@@ -37,7 +37,7 @@ def main():
     t1 = None
     for N in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
         owner = ge.assign_aggregates(PT, L[0], N)
-        times, reps = [], []
+        times, reps, scheds = [], [], []
         for r in range(N):
             mine = np.flatnonzero(owner == r).astype(np.int32)
             p = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
@@ -52,9 +52,11 @@ def main():
             times.append((time.perf_counter() - t0) / iters * 1e3)
             rep_ms, _, _ = p.repulse_ms()
             reps.append(rep_ms)
+            scheds.append(p.schedule())
             p.close()
         t1 = t1 or times[0]
         print(json.dumps({"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times), "repulse_ms_by_rank": reps,
+                          "schedule_by_rank": scheds,
                           "efficiency": t1 / (N * max(times))}), flush=True)
     ctx.close()
 

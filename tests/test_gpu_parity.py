@@ -261,13 +261,20 @@ def test_fa_small_level_graph_replay(ctx, oracle):
 
 @pytest.mark.parametrize("n,dim,grp,its", [(300, 3, "0", 200), (700, 2, "0", 131),
                                             (1300, 4, "0", 128), (2900, 3, "32", 129),
-                                            (1068, 3, "16", 140), (500, 1, "64", 257)])
+                                            (1068, 3, "16", 140), (500, 1, "64", 257),
+                                            (1068, 3, "nopack", 131), (97, 4, "0", 129),
+                                            (1999, 2, "0", 128)])
 def test_fa_persistent_small_level(ctx, oracle, monkeypatch, n, dim, grp, its):
     """Small levels with >= 128 iterations run every iteration in one launch
     (fa_grouped_persistent: resident blocks, grid barrier, coordinates in two
-    alternating buffers); odd and even counts, G lanes per row."""
+    alternating buffers); odd and even counts, G lanes per row.  At 64 lanes per
+    row the rows are packed (packed_iteration: one adder wave, three producer
+    waves; ragged last block, rows of degree above one chunk); "nopack" keeps one
+    wave per row."""
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
-    if grp != "0":
+    if grp == "nopack":
+        monkeypatch.setenv("GE_FA_PACKED", "0")
+    elif grp != "0":
         monkeypatch.setenv("GE_GRP_G", grp)
     A = G.rmat(n, 6 * n, seed=n + dim)
     X0 = G.random_coords(n, dim, seed=n)
@@ -313,7 +320,7 @@ def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("grp", ["0", "16", "32"])
+@pytest.mark.parametrize("grp", ["0", "nopack", "16", "32"])
 def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     """The coarsest level at its production size and horizon: an R-MAT LCC coarsened
     twice by partition(A, 0.125) (n = 1067, integer weights, self-loops), seeded
@@ -321,7 +328,9 @@ def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     grid-barrier kernel, against the oracle's run of the same 1e5 iterations
     (tests/golden/make_coarsest_1e5.py)."""
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
-    if grp != "0":
+    if grp == "nopack":  # 64 lanes per row, one wave per row (grouped_iteration)
+        monkeypatch.setenv("GE_FA_PACKED", "0")
+    elif grp != "0":
         monkeypatch.setenv("GE_GRP_G", grp)
     g = golden("fa_coarsest_1e5")
     A = (g["A_ip"], g["A_ix"], g["A_dx"])
