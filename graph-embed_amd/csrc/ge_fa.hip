@@ -838,8 +838,14 @@ __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
 // acquire fence after the poll; 3 acquire fence only and plain (L2-cached) staging
 // loads; 4 release + acquire and plain staging loads.  The coordinates are always
 // stored with agent-scope stores.
+// Measured (n = 919, 20 000 iterations, one box, scripts/coarsest_time.py,
+// profiles/r04/coarsest_barrier_variants.log): packed rows 17.9 / 20.6 / 18.8 /
+// 20.0 us per iteration for orders 0 / 2 / 3 / 4 -- the release write-back and
+// the acquire invalidate each cost more than the whole barrier's ordering is worth
+// here, so the shipped order is 0: agent-scope (L2-bypassing) stores and loads of
+// the coordinates, every store completed (s_waitcnt 0) before the arrival.
 #ifndef GE_BAR_ORDER
-#define GE_BAR_ORDER 2
+#define GE_BAR_ORDER 0
 #endif
 constexpr bool kBarCohStage = GE_BAR_ORDER < 3;
 
@@ -1634,7 +1640,7 @@ static void plan_init(ge_fa_plan* pl) {
     pl->sym_units = T;
     pl->units.alloc(T);
     pl->units.upload(h_units.data(), T, s);
-    pl->ctl.alloc(1 + 2 * T);  // queue, progress counters, (unused) band flags
+    pl->ctl.alloc(1 + T);  // queue, progress counters
     const int h_seg[2] = {0, pl->n};
     pl->seg.alloc(2);
     pl->seg.upload(h_seg, 2, s);
@@ -1730,8 +1736,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
       GE_HIP(hipMemsetAsync(pl->ctl.p, 0, sizeof(int) * pl->ctl.n, s));
       sym_repulse_launch(D, pl->sym_blocks, s, pl->sym_units, pl->units.p, pl->ctl.p,
                          pl->seg.p, xc, pl->dp1.p, pl->p.repel, pl->frep.p, pl->hand.p,
-                         (size_t)pl->n, pl->ctl.p + 1, pl->sym_units, pl->sym_err_d,
-                         pl->sym_limit);
+                         (size_t)pl->n, pl->ctl.p + 1, pl->sym_err_d, pl->sym_limit);
     } else {
       launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
                           pl->frep.p, pl->fpart.p, pl->cus);

@@ -943,12 +943,14 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // chain) tile-times, where
     //   sweeps:  work T^2 / 2 + T,               chain chain_k T
     //   K bands: work sum_b (Tb^2 / 2 + Tb) + row_k sum_b Tb (T - Tb),
-    //            chain max_b (row_k b0 + chain_k Tb + row_k (T - b1))
+    //            chain max_b (row_k b0 + chain_k Tb + row_k (T - b1)), the post
+    //            part run by each sweep's own wave after its band
     //   rows:    work row_k T^2,                 chain row_k T
     // (a row block evaluates every ordered pair at ~0.8 the step cost of a sweep; a
     // sweep chain is ~2.5 T because each sweep starts ~2 tiles behind the one before).
-    // Row-block units (whole, pre) are first in the queue, so when they hold more than
-    // the waves the sweeps start late (start = their work / waves).  Greedy: while the
+    // Whole row blocks are first in the queue, so when they hold more than the waves
+    // the sweeps start late (start = their work / waves); the pre blocks of a band
+    // are interleaved with the sweeps, each just ahead of when its column tile is due.  Greedy: while the
     // longest chain sets the time, step its aggregate to the next option (more bands,
     // then rows) if that lowers the prediction.  At N = 1 (C4) the launch is
     // work-bound and nothing changes; the shares of a multi-GPU run are chain-bound.
@@ -970,7 +972,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       for (int i = 0; i < K; ++i) {
         const double b0 = band_lo(Tb, K, i), b1 = band_lo(Tb, K, i + 1), tb = b1 - b0;
         work += 0.5 * tb * tb + tb + row_k * tb * (t - tb);
-        rwork += row_k * tb * b0;  // the pre blocks (first in the queue)
         chain = std::max(chain, row_k * b0 + chain_k * tb + row_k * (t - b1));
       }
     };
@@ -990,7 +991,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         cost_of(T[b], K, w, c, r);
         work += w;
         rwork += r;
-        if (K != 1) runits += K == kRowsMode ? T[b] : T[b] - band_lo(T[b], K, 1);
+        if (K == kRowsMode) runits += T[b];  // whole row blocks: first in the queue
         ch[b] = c;
       }
       const double start = runits > waves ? rwork / waves : 0.0;
@@ -1082,14 +1083,16 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         for (int i = 0; i < K; ++i) {
           const int b0 = band_lo(T[b], K, i), b1 = band_lo(T[b], K, i + 1);
           const bool last = i + 1 == K;
+          const double e0 = row_k * b0 * sc;  // the band's first sweep
           for (int A = b0; A < b1; ++A) {
+            // the pre block of tile A is due when the band's first sweep reaches
+            // column tile A; all of the band's pre blocks stay ahead of that sweep
+            // in the queue (a unit waits only on units before it)
             if (b0 > 0)
-              rows_units.push_back({big[b], A, pb, T[b], unit_word(kUnitPre, b0, b1), -1.0});
-            const double e = (row_k * b0 + est_k * (A - b0)) * sc;
-            us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, b0, last ? 0 : b1), e});
-            if (!last)
-              us.push_back({big[b], A, pb, T[b], unit_word(kUnitPost, b0, b1),
-                            e + (b1 - A) * sc});
+              us.push_back({big[b], A, pb, T[b], unit_word(kUnitPre, b0, b1),
+                            std::min((A - b0) * sc, e0 - 1e-3) - 1e-3});
+            us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, b0, last ? 0 : b1),
+                          e0 + est_k * (A - b0) * sc});
           }
         }
       }
@@ -1120,7 +1123,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       pl->h_units = h_units;
       pl->stamps.alloc(h_units.size() * kStampWords);
     }
-    pl->prog.alloc(std::max(2 * pb, 1));  // progress counters, then the bands' rdone flags
+    pl->prog.alloc(std::max(pb, 1));
     if (pb > 0) pl->hand.alloc((size_t)pl->n * dim);
     pl->sym_err.alloc(1);
     GE_HIP(hipMemsetAsync(pl->sym_err.p, 0, sizeof(int), st));
@@ -1264,7 +1267,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           GE_HIP(hipEventRecord(re[0], ss));
         }
         if (pl->sym) {
-          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * 2 * pl->ntiles, ss));
+          if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
           double* H = pl->hand.p;
           const size_t hs = (size_t)pl->n;
           int* err = pl->sym_err.p;
@@ -1292,17 +1295,17 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               pl->ntiles, err, lim, pl->stamps.p);
+                               err, lim, pl->stamps.p);
 #endif
           } else if (!pl->stamp_path.empty()) {
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               pl->ntiles, err, lim, pl->stamps.p);
+                               err, lim, pl->stamps.p);
           } else {
             sym_repulse_launch(D, pl->sym_blocks, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               pl->ntiles, err, lim);
+                               err, lim);
           }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
@@ -1383,25 +1386,26 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
 
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
-                        double repel, double* F, double* H, size_t hs, int* prog, int ptiles,
-                        int* err, long long limit) {
+                        double repel, double* F, double* H, size_t hs, int* prog, int* err,
+                        long long limit) {
   dispatch_dim(dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
     if (repel == 1.0)
       hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(blocks), dim3(kSymT), 0, s, nunits,
-                         units, queue, seg, X, DP, repel, F, H, hs, prog, ptiles, err, limit,
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit,
                          nullptr);
     else
       hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(blocks), dim3(kSymT), 0, s, nunits,
-                         units, queue, seg, X, DP, repel, F, H, hs, prog, ptiles, err, limit,
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit,
                          nullptr);
   });
   GE_HIP(hipGetLastError());
 }
 
-// three blocks (waves) per SIMD of the four that fit: fewer units in flight spin
-// less on hand-overs (C4 N = 1: 137.2 against 138.3 ms per launch; N = 8 shares
-// 30.0 against 32.7 ms; scripts/sym_timeline.py, profiles/r03/sym_timeline)
+// Blocks per CU of a single-level symmetric launch (one aggregate of n / 64 row
+// tiles: one convoy of sweeps, each behind the one before).  Two of the four that
+// fit: C2 1539.8 ms per iteration against 1631.9 at three and 1806.8 at four
+// (profiles/r04/c2_sym_blocks.log) -- fewer sweeps in flight wait less on each other.
 int sym_blocks_per_cu(int dim) {
   int occ = 1;
   dispatch_dim(dim, [&](auto Dc) {
@@ -1409,7 +1413,7 @@ int sym_blocks_per_cu(int dim) {
     GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
   });
-  return std::min(std::max(occ, 1), 3);
+  return std::min(std::max(occ, 1), 2);
 }
 
 static void faml_plan_free(ge_faml_plan* pl) {

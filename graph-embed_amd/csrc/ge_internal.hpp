@@ -163,8 +163,8 @@ void check_csr(int n, const int* ip, const int* ix, const double* dx);
 // forceAtlas (ge_fa.hip).  sym_blocks_per_cu: the resident blocks it is sized for.
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
-                        double repel, double* F, double* H, size_t hs, int* prog, int ptiles,
-                        int* err, long long limit);
+                        double repel, double* F, double* H, size_t hs, int* prog, int* err,
+                        long long limit);
 int sym_blocks_per_cu(int dim);
 
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,

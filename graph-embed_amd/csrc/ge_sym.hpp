@@ -218,15 +218,15 @@ __device__ __forceinline__ void sym_steps_any(bool fast, int s0, int s1, int lan
 
 // A row block: the 64 rows of tile A against the members [c0, c1) in ascending
 // order, every pair evaluated for its row (the plain ordered-pair scheme: no
-// dependencies besides the start value).  acc starts at +0 or, with from_F, at the
-// rows' sums in F (agent-scope loads: another XCD's wave wrote them).  Used for
-// whole aggregates whose sweep chain would outlast the launch (c0 = 0, c1 = s) and
-// for the cross-band parts of banded aggregates (see faml_sym_repulse).
+// dependencies besides the start value).  acc starts at +0 (fresh) or continues
+// the rows' sums passed in.  Used for whole aggregates whose sweep chain would
+// outlast the launch (c0 = 0, c1 = s) and for the cross-band parts of banded
+// aggregates (see faml_sym_repulse).
 template <int D, bool REPEL_ONE>
 __device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int c0, int c1,
-                                           bool from_F, const double* X, const double* DP,
+                                           bool fresh, const double* X, const double* DP,
                                            double repel, bool repel_ok, double* tile,
-                                           const double* F, double (&acc)[D]) {
+                                           double (&acc)[D]) {
   constexpr int WV = SymW<D>::v;
   const size_t rb = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
@@ -234,7 +234,7 @@ __device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     xi[k] = rv ? X[(rb + lane) * D + k] : 0.0;
-    acc[k] = (rv && from_F) ? agent_ld(F + (rb + lane) * D + k) : 0.0;
+    if (fresh) acc[k] = 0.0;
   }
   if (rv) di = DP[rb + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xi, di));
@@ -268,7 +268,7 @@ __device__ __forceinline__ void rows_block(int lane, int base, int s, int A, con
                                            const double* DP, double repel, bool repel_ok,
                                            double* tile, double* F) {
   double acc[D];
-  rows_range<D, REPEL_ONE>(lane, base, s, A, 0, s, false, X, DP, repel, repel_ok, tile, F, acc);
+  rows_range<D, REPEL_ONE>(lane, base, s, A, 0, s, true, X, DP, repel, repel_ok, tile, acc);
   if (64 * A + lane < s) {
     const size_t rb = (size_t)base + 64 * (size_t)A;
 #pragma unroll
@@ -294,8 +294,8 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
                                            double* __restrict__ H, size_t hs, int* err,
                                            long long limit, bool& give_up, double* rec,
                                            double* ini, double* out, long long& spin,
-                                           long long& t_first, int cend = 0,
-                                           int* rdone = nullptr) {
+                                           long long& t_first, int cend,
+                                           double (&rout)[D]) {
   constexpr int IW = SymI<D>::v;
   const size_t cbase = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
@@ -372,21 +372,10 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
                                        xr, dr, rv, repel, racc, flow);
   if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
-  if (rdone) {
-    // a band before the last: the rows' sums continue in a post row block on
-    // another wave (another XCD): agent-scope stores, completed before the flag
-    if (rv) {
+  // the rows' sums: the caller writes them to F, or (a band before the last)
+  // continues them with the members after the band
 #pragma unroll
-      for (int k = 0; k < D; ++k) agent_st(F + (cbase + lane) * D + k, racc[k]);
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) __hip_atomic_store(rdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (rv) {
-#pragma unroll
-    for (int k = 0; k < D; ++k) F[(cbase + lane) * D + k] = racc[k];
-  }
+  for (int k = 0; k < D; ++k) rout[k] = racc[k];
 }
 
 // Stamp record of one unit (STAMP builds): see kStampWords.
@@ -411,20 +400,21 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
 //         are set to b0;
 //   sweeps (kind 0, band end b1): the band's rows and columns symmetric, each row
 //         continuing from its column sum at the diagonal as before;
-//   post  (kind 4): the band's rows against the members after the band, as a row
-//         block starting from the sweep's row sums (flag rdone[A]).
+//   post: the same wave, once its band sweep is done, continues its rows against
+//         the members after the band as a row block (the row sums stay in
+//         registers; the sweep's hand-overs all happened in the band part).
 // The chain of band b is ~0.8 b0 + 2.5 (b1 - b0) + 0.8 (T - b1) tile-times; the
 // cross-band pairs are evaluated twice (ordered), the in-band pairs once.
-constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3, kUnitPost = 4;
+constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3;
 __host__ __device__ inline int unit_word(int kind, int b0, int b1) {
   return kind | (b0 << 4) | (b1 << 18);
 }
 constexpr int kUnitMaxTile = (1 << 14) - 1;  // band tile indices are 14-bit fields
 
 // units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
-// unit_word(kind, band first tile, band end tile)} in queue order; prog (2 x
-// ptiles: progress counters, then the rdone flags) zeroed before the launch;
-// queue = one counter.  Every unit waits only on units before it in the queue.
+// unit_word(kind, band first tile, band end tile)} in queue order; prog (ptiles
+// progress counters) zeroed before the launch; queue = one counter.  Every unit
+// waits only on units before it in the queue.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
 // (diagnostics, wrong results): no sweep waits for its hand-overs.
 template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
@@ -432,7 +422,7 @@ __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
-                 double* __restrict__ H, size_t hs, int* __restrict__ prog, int ptiles,
+                 double* __restrict__ H, size_t hs, int* __restrict__ prog,
                  int* __restrict__ err, long long limit, long long* __restrict__ stamps) {
   constexpr int WV = SymW<D>::v;
   constexpr int IW = SymI<D>::v;
@@ -468,8 +458,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     } else if (kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
       __builtin_amdgcn_s_setprio(3);
       double acc[D];
-      rows_range<D, REPEL_ONE>(lane, base, s, A, 0, 64 * b0, false, X, DP, repel, repel_ok, rec,
-                               F, acc);
+      rows_range<D, REPEL_ONE>(lane, base, s, A, 0, 64 * b0, true, X, DP, repel, repel_ok, rec,
+                               acc);
       __builtin_amdgcn_s_setprio(0);
       if (64 * A + lane < s) {
 #pragma unroll
@@ -480,26 +470,23 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0)
         __hip_atomic_store(prog + u.z + A, b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (kind == kUnitPost) {  // the band's rows after its sweeps
-      handover_wait<false>(prog + ptiles + u.z + A, 1, err, limit, give_up);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_setprio(3);
-      double acc[D];
-      rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b1, s, true, X, DP, repel, repel_ok, rec,
-                               F, acc);
-      __builtin_amdgcn_s_setprio(0);
-      if (64 * A + lane < s) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = acc[k];
-      }
     } else {
-      // a sweep; in a band that is not the aggregate's last, stop at the band's end
-      // and hand the row sums to the post block
+      // a sweep; in a band that is not the aggregate's last it stops at the band's
+      // end and the same wave continues its rows past the band (post)
       const bool banded = b1 > 0 && 64 * b1 < s;
+      double racc[D];
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, ini,
-                                              out, spin, t_first, banded ? 64 * b1 : 0,
-                                              banded ? prog + ptiles + u.z + A : nullptr);
+                                              out, spin, t_first, banded ? 64 * b1 : 0, racc);
+      if (banded) {
+        wave_lds_sync();  // the rings are free: the row block stages its tiles in rec
+        rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b1, s, false, X, DP, repel, repel_ok,
+                                 rec, racc);
+      }
+      if (64 * A + lane < s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = racc[k];
+      }
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
