@@ -1633,30 +1633,6 @@ static void plan_init(ge_fa_plan* pl) {
     pl->sym = !off && pl->p.mode == GE_MODE_STRICT && pl->rb == 0 && pl->re == pl->n &&
               (force || pl->n > stream_max());
   }
-  if (pl->sym) {
-    const int T = (pl->n + 63) / 64;
-    std::vector<int4> h_units(T);
-    for (int A = 0; A < T; ++A) h_units[A] = make_int4(0, A, 0, 0);  // earliest start 2A
-    pl->sym_units = T;
-    pl->units.alloc(T);
-    pl->units.upload(h_units.data(), T, s);
-    pl->ctl.alloc(1 + T);  // queue, progress counters
-    const int h_seg[2] = {0, pl->n};
-    pl->seg.alloc(2);
-    pl->seg.upload(h_seg, 2, s);
-    pl->hand.alloc((size_t)pl->n * pl->dim);
-    pl->sym_blocks = pl->cus * sym_blocks_per_cu(pl->dim);
-    if (const char* e = std::getenv("GE_FA_SYM_BLOCKS"))  // tuning: blocks per CU
-      pl->sym_blocks = pl->cus * std::max(1, std::min(4, std::atoi(e)));
-    int dev = 0, khz = 0;
-    GE_HIP(hipGetDevice(&dev));
-    GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-    pl->sym_limit = (long long)std::max(khz, 1000) * 5000;  // ~5 s per hand-over wait
-    GE_HIP(hipHostMalloc((void**)&pl->sym_err_h, sizeof(int), hipHostMallocMapped));
-    *pl->sym_err_h = 0;
-    GE_HIP(hipHostGetDevicePointer((void**)&pl->sym_err_d, pl->sym_err_h, 0));
-    GE_HIP(hipStreamSynchronize(s));
-  }
   // Gather copy, opt-in (GE_GATHER_COPY=1).  Measured without benefit: C2 attraction
   // 0.324 ms with it against 0.301 ms without, C5 31.8 against 30.3 ms; L2 misses
   // fell 14 % (FETCH 697 MB per C2 pass) but the long tail of low-degree
@@ -1685,6 +1661,37 @@ static void plan_init(ge_fa_plan* pl) {
       hipLaunchKernelGGL(remap_indices_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
                          cnt, dpos.p, pl->ix + pl->gbase, pl->gix.p);
     GE_HIP(hipGetLastError());
+    GE_HIP(hipStreamSynchronize(s));
+  }
+}
+
+// The symmetric path's units, progress counters and hand-over buffer (n x d), made
+// on the plan's first step (a plan used only for its row kernels never needs them).
+static void sym_prepare(ge_fa_plan* pl) {
+  if (!pl->sym || pl->sym_units > 0) return;
+  hipStream_t s = pl->ctx->stream;
+  {
+    const int T = (pl->n + 63) / 64;
+    std::vector<int4> h_units(T);
+    for (int A = 0; A < T; ++A) h_units[A] = make_int4(0, A, 0, 0);  // earliest start 2A
+    pl->sym_units = T;
+    pl->units.alloc(T);
+    pl->units.upload(h_units.data(), T, s);
+    pl->ctl.alloc(1 + T);  // queue, progress counters
+    const int h_seg[2] = {0, pl->n};
+    pl->seg.alloc(2);
+    pl->seg.upload(h_seg, 2, s);
+    pl->hand.alloc((size_t)pl->n * pl->dim);
+    pl->sym_blocks = pl->cus * sym_blocks_per_cu(pl->dim);
+    if (const char* e = std::getenv("GE_FA_SYM_BLOCKS"))  // tuning: blocks per CU
+      pl->sym_blocks = pl->cus * std::max(1, std::min(4, std::atoi(e)));
+    int dev = 0, khz = 0;
+    GE_HIP(hipGetDevice(&dev));
+    GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    pl->sym_limit = (long long)std::max(khz, 1000) * 5000;  // ~5 s per hand-over wait
+    GE_HIP(hipHostMalloc((void**)&pl->sym_err_h, sizeof(int), hipHostMallocMapped));
+    *pl->sym_err_h = 0;
+    GE_HIP(hipHostGetDevicePointer((void**)&pl->sym_err_d, pl->sym_err_h, 0));
     GE_HIP(hipStreamSynchronize(s));
   }
 }
@@ -1732,6 +1739,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
       return;
     }
     if (pl->sym) {
+      sym_prepare(pl);
       sym_check(pl);
       GE_HIP(hipMemsetAsync(pl->ctl.p, 0, sizeof(int) * pl->ctl.n, s));
       sym_repulse_launch(D, pl->sym_blocks, s, pl->sym_units, pl->units.p, pl->ctl.p,
@@ -1931,6 +1939,7 @@ void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix
   pl.p = p;
   pl.c = make_const(p);
   plan_init(&pl);
+  sym_prepare(&pl);  // before any graph capture below
   DevBuf<double> other((size_t)n * dim);
   double* cur = d_x;
   double* nxt = other.p;

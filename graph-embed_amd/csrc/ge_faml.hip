@@ -1006,6 +1006,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       return std::max(work / waves, chain);
     };
     double best = any_big ? predict(nullptr) : 0.0;
+    // GE_FAML_SYM_NOBANDS=1: plain sweeps or whole row blocks only (comparisons)
+    const bool no_bands = std::getenv("GE_FAML_SYM_NOBANDS") && *std::getenv("GE_FAML_SYM_NOBANDS") == '1';
     if (chain_k > 0.0 && any_big && force_bands == 0) {
       const int nopt = sizeof(kOptions) / sizeof(kOptions[0]);
       for (;;) {
@@ -1014,7 +1016,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         // sweep pairs have no banded form; bands need 2 tiles each and 14-bit indices
         int next = opt[crit] + 1;
         while (next < nopt && kOptions[next] != kRowsMode &&
-               (pl->sym_pair || kOptions[next] > T[crit] / 2 || T[crit] > kUnitMaxTile))
+               (pl->sym_pair || no_bands || kOptions[next] > T[crit] / 2 ||
+                T[crit] > kUnitMaxTile))
           ++next;
         if (next >= nopt) break;
         const int keep = opt[crit];
