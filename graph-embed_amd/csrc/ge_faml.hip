@@ -976,6 +976,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       }
     };
     static const int kOptions[] = {1, 2, 3, 4, 6, 8, kRowsMode};
+    constexpr int kRowSegTiles = 96;  // column tiles per segment of a row block
     std::vector<int> opt(big.size(), 0);  // index into kOptions
     auto mode_of = [&](size_t b) {
       if (force_bands > 0) return std::min(force_bands, std::max(1, T[b] / 2));
@@ -1006,9 +1007,47 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       return std::max(work / waves, chain);
     };
     double best = any_big ? predict(nullptr) : 0.0;
-    // GE_FAML_SYM_NOBANDS=1: plain sweeps or whole row blocks only (comparisons)
+    // Default: the round-3 rule -- the k largest aggregates as whole row blocks, k
+    // minimising max(work / waves, row path, sweeps' start + chain), and no mix
+    // whose row blocks hold more than half the waves (their raised waves delay and
+    // slow the sweeps: measured on per-rank shares of C4, N = 4: 20 of 24 aggregates
+    // as row blocks 70 ms per iteration, 7 of 25 58 ms).  Bands and the greedy below
+    // are opt-in (GE_FAML_SYM_BANDED=1): on the same one-GPU rehearsal they were
+    // slower (N = 4 / 8 shares 74 / 49 ms against 57 / 30 ms,
+    // profiles/r04/scale_sim_c4_bands.log).
+    const bool banded_greedy =
+        std::getenv("GE_FAML_SYM_BANDED") && *std::getenv("GE_FAML_SYM_BANDED") == '1';
+    if (chain_k > 0.0 && any_big && force_bands == 0 && !banded_greedy) {
+      std::vector<size_t> by_T(big.size());
+      std::iota(by_T.begin(), by_T.end(), 0);
+      std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
+      double work = 0.0, row_work = 0.0, row_units = 0.0, pbest = 1e300;
+      size_t best_k = 0;
+      for (size_t b = 0; b < big.size(); ++b) work += 0.5 * T[b] * (double)T[b] + T[b];
+      for (size_t k = 0; k <= by_T.size(); ++k) {  // the k largest as row blocks
+        const double start = row_units > waves ? row_work / waves : 0.0;
+        const double sweep_chain = k < by_T.size() ? start + chain_k * T[by_T[k]] : 0.0;
+        const double row_path = k > 0 ? row_k * T[by_T[0]] : 0.0;
+        const double pred = std::max(work / waves, std::max(sweep_chain, row_path));
+        const bool mixed_late = 2.0 * row_units > waves && k < by_T.size();
+        if (!mixed_late && pred < pbest * 0.999) {
+          pbest = pred;
+          best_k = k;
+        }
+        if (k < by_T.size()) {
+          const double t = T[by_T[k]];
+          work += 0.8 * t * t - (0.5 * t * t + t);
+          row_work += 0.8 * t * t;
+          row_units += t;
+        }
+      }
+      const int nopt_rows = sizeof(kOptions) / sizeof(kOptions[0]) - 1;  // kRowsMode
+      for (size_t k = 0; k < best_k; ++k) opt[by_T[k]] = nopt_rows;
+      best = pbest;
+    }
+    // GE_FAML_SYM_NOBANDS=1 (with the greedy): plain sweeps or whole row blocks only
     const bool no_bands = std::getenv("GE_FAML_SYM_NOBANDS") && *std::getenv("GE_FAML_SYM_NOBANDS") == '1';
-    if (chain_k > 0.0 && any_big && force_bands == 0) {
+    if (chain_k > 0.0 && any_big && force_bands == 0 && banded_greedy) {
       const int nopt = sizeof(kOptions) / sizeof(kOptions[0]);
       for (;;) {
         size_t crit = 0;
@@ -1071,8 +1110,23 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     for (size_t b = 0; b < big.size(); ++b) {
       const int K = mode_of(b);
       if (K == kRowsMode) {
-        for (int A = 0; A < T[b]; ++A)
-          rows_units.push_back({big[b], A, 0, T[b], unit_word(kUnitRows, 0, 0), -1.0});
+        // segments of about kRowSegTiles column tiles (GE_FAML_ROWSEG overrides; 0:
+        // whole row blocks), layer g after layer g - 1 in the queue
+        int seg = kRowSegTiles;
+        if (const char* e = std::getenv("GE_FAML_ROWSEG")) seg = std::max(0, std::atoi(e));
+        const int G = seg > 0 && T[b] <= kUnitMaxTile ? std::max(1, (T[b] + seg - 1) / seg) : 1;
+        if (G == 1) {
+          for (int A = 0; A < T[b]; ++A)
+            rows_units.push_back({big[b], A, 0, T[b], unit_word(kUnitRows, 0, 0), -1.0});
+        } else {
+          for (int g = 0; g < G; ++g) {
+            const int c0 = (int)((long long)T[b] * g / G), c1 = (int)((long long)T[b] * (g + 1) / G);
+            for (int A = 0; A < T[b]; ++A)
+              rows_units.push_back({big[b], A, pb, T[b], unit_word(kUnitRowSeg, c0, c1),
+                                    -1.0 + 1e-6 * g});
+          }
+          pb += T[b];  // the row tiles' progress counters
+        }
         continue;
       }
       const double sc = scale_of(T[b]);

@@ -405,7 +405,14 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
 //         registers; the sweep's hand-overs all happened in the band part).
 // The chain of band b is ~0.8 b0 + 2.5 (b1 - b0) + 0.8 (T - b1) tile-times; the
 // cross-band pairs are evaluated twice (ordered), the in-band pairs once.
-constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3;
+// Segmented row blocks (kind 5): a row tile's row block cut into column segments
+// [c0, c1) of tiles, run as separate units in layers (every row tile's first
+// segment, then every second, ...); a segment continues the rows' sums of the one
+// before (F, agent scope; progress counter = the segment's first column tile).  A
+// whole row block is T tiles of one wave; the last ones taken set the launch's
+// tail (N = 8 share of C4: queue drained at 17.9 ms, last block ended at 28.3 ms,
+// profiles/r04/sym_timeline_rows_n8.json), a segment only T / G tiles.
+constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3, kUnitRowSeg = 5;
 __host__ __device__ inline int unit_word(int kind, int b0, int b1) {
   return kind | (b0 << 4) | (b1 << 18);
 }
@@ -455,6 +462,34 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
+    } else if (kind == kUnitRowSeg) {  // columns [64 b0, 64 b1) of row tile A's row block
+      const bool first = b0 == 0, last = 64 * b1 >= s;
+      double acc[D];
+      if (!first) {  // the segment before has stored the rows' sums
+        handover_wait<false>(prog + u.z + A, b0, err, limit, give_up);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          acc[k] = 64 * A + lane < s ? agent_ld(F + (rb + lane) * D + k) : 0.0;
+      }
+      __builtin_amdgcn_s_setprio(3);
+      rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b0, min(64 * b1, s), first, X, DP, repel,
+                               repel_ok, rec, acc);
+      __builtin_amdgcn_s_setprio(0);
+      if (64 * A + lane < s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          if (last) F[(rb + lane) * D + k] = acc[k];
+          else agent_st(F + (rb + lane) * D + k, acc[k]);
+        }
+      }
+      if (!last) {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0)
+          __hip_atomic_store(prog + u.z + A, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else if (kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
       __builtin_amdgcn_s_setprio(3);
       double acc[D];

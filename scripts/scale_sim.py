@@ -40,6 +40,12 @@ def main():
         times, reps, scheds = [], [], []
         for r in range(N):
             mine = np.flatnonzero(owner == r).astype(np.int32)
+            # STAMP_N=N: the per-unit timeline of rank 0's last launch (GE_SYM_STAMPS,
+            # scripts/sym_timeline.py) into gpurun_out/stamps_N<N>.bin
+            if os.environ.get("STAMP_N") == str(N) and r == 0:
+                os.environ["GE_SYM_STAMPS"] = os.path.join(REPO, "gpurun_out", f"stamps_N{N}.bin")
+            else:
+                os.environ.pop("GE_SYM_STAMPS", None)
             p = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
                             PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
                             dim, iterations=iters, aggs=mine if N > 1 else None)

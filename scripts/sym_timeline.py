@@ -65,8 +65,17 @@ def analyse(path):
     out["latest_aggregates"] = [{"agg": a, "tiles": v[2], "kind": v[4], "first_take_ms": v[0] / 1e3,
                                  "last_end_ms": v[1] / 1e3, "spin_ms_sum": v[3] / 1e3} for a, v in crit]
     # per-tile time of the sweeps: duration / tiles processed
-    sw = units[:, 3] == 0
+    kind = units[:, 3] & 15  # ge_sym.hpp unit_word: kind | band first tile << 4 | band end << 18
+    sw = kind == 0
     out["sweep_unit_us_median"] = float(np.median(dur[sw])) if sw.any() else None
+    for name, k in (("sweep", 0), ("rows", 1), ("pre", 3)):
+        sel = kind == k
+        if sel.any():
+            out[f"{name}_units"] = {"count": int(sel.sum()), "dur_us_median": float(np.median(dur[sel])),
+                                    "dur_ms_sum": float(dur[sel].sum() / 1e3),
+                                    "spin_ms_sum": float(spin[sel].sum() / 1e3),
+                                    "last_end_ms": float(end[sel].max() / 1e3),
+                                    "first_take_ms": float(take[sel].min() / 1e3)}
     # per SIMD (HW_ID bits: wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13; XCC_ID low bits)
     hw = st[:, 4]
     simd = (st[:, 5] & 0xF) * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15) * 16 + ((hw >> 4) & 3)

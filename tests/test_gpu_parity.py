@@ -558,6 +558,28 @@ def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("seg,dim,repel", [("4", 3, 1.0), ("7", 3, 2.0 ** 70), ("3", 2, 1.5),
+                                           ("5", 4, 1.0), ("1", 3, 1.0)])
+def test_faml_segmented_row_blocks(ctx, oracle, monkeypatch, seg, dim, repel):
+    """Row blocks cut into column segments of `seg` tiles (ge_sym.hpp kind 5): each
+    segment continues its rows' sums from the one before through F, layer after
+    layer in the queue; ragged last segments, one-tile segments, the `/` path."""
+    monkeypatch.setenv("GE_FAML_SYM", "1")
+    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "1e9")  # every streamed aggregate as row blocks
+    monkeypatch.setenv("GE_FAML_ROWSEG", seg)
+    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=17), [(3, 2000), (70, 3000)], seed=dim)
+    PT = _block_partition(n, sizes, seed=7)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m + 2)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=29, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=29, repel=repel)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("bands,dim,repel", [
     ("2", 3, 1.0), ("3", 3, 1.0), ("4", 3, 1.5), ("8", 3, 1.0), ("2", 3, 2.0 ** 70),
     ("3", 2, 1.0), ("4", 4, 0.75), ("2", 1, 1.0)])
