@@ -946,8 +946,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     //            chain max_b (row_k b0 + chain_k Tb + row_k (T - b1)), the post
     //            part run by each sweep's own wave after its band
     //   rows:    work row_k T^2,                 chain row_k T
-    // (a row block evaluates every ordered pair at ~0.8 the step cost of a sweep; a
-    // sweep chain is ~2.5 T because each sweep starts ~2 tiles behind the one before).
+    // (a row block evaluates every ordered pair at ~0.6 the wave time of a sweep tile;
+    // a sweep chain is ~2.5 T because each sweep starts ~2 tiles behind the one before).
     // Whole row blocks are first in the queue, so when they hold more than the waves
     // the sweeps start late (start = their work / waves); the pre blocks of a band
     // are interleaved with the sweeps, each just ahead of when its column tile is due.  Greedy: while the
@@ -955,7 +955,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // then rows) if that lowers the prediction.  At N = 1 (C4) the launch is
     // work-bound and nothing changes; the shares of a multi-GPU run are chain-bound.
     constexpr int kRowsMode = 1 << 20;
-    double chain_k = 2.5, row_k = 0.8;
+    // row_k: a row-block tile (64 x 64 ordered pairs) against a sweep tile (64 x 64
+    // unordered), wave time at full load -- 0.6 measured on an N = 8 share of C4
+    // (all row blocks: 17.9 us per row tile per wave, against 29.8 us per sweep tile
+    // at N = 1; profiles/r04/sym_timeline_rows_n8.json)
+    double chain_k = 2.5, row_k = 0.6;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
     int force_bands = 0;  // GE_FAML_SYM_BANDS=K: every streamed aggregate in K bands (tests)
@@ -1036,8 +1040,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         }
         if (k < by_T.size()) {
           const double t = T[by_T[k]];
-          work += 0.8 * t * t - (0.5 * t * t + t);
-          row_work += 0.8 * t * t;
+          work += row_k * t * t - (0.5 * t * t + t);
+          row_work += row_k * t * t;
           row_units += t;
         }
       }
