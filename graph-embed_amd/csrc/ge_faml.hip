@@ -980,7 +980,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       }
     };
     static const int kOptions[] = {1, 2, 3, 4, 6, 8, kRowsMode};
-    constexpr int kRowSegTiles = 96;  // column tiles per segment of a row block
     std::vector<int> opt(big.size(), 0);  // index into kOptions
     auto mode_of = [&](size_t b) {
       if (force_bands > 0) return std::min(force_bands, std::max(1, T[b] / 2));
@@ -1114,9 +1113,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     for (size_t b = 0; b < big.size(); ++b) {
       const int K = mode_of(b);
       if (K == kRowsMode) {
-        // segments of about kRowSegTiles column tiles (GE_FAML_ROWSEG overrides; 0:
-        // whole row blocks), layer g after layer g - 1 in the queue
-        int seg = kRowSegTiles;
+        // whole row blocks by default; GE_FAML_ROWSEG=t cuts them into column segments
+        // of about t tiles, layer g after layer g - 1 in the queue (N = 8 shares of C4:
+        // the tail shrank from 10.4 to 3.6 ms but the launch did not, 33.7 against
+        // 31.5 ms per iteration, profiles/r04/scale_sim_c4_rows_seg.log)
+        int seg = 0;
         if (const char* e = std::getenv("GE_FAML_ROWSEG")) seg = std::max(0, std::atoi(e));
         const int G = seg > 0 && T[b] <= kUnitMaxTile ? std::max(1, (T[b] + seg - 1) / seg) : 1;
         if (G == 1) {

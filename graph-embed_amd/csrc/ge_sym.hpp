@@ -405,13 +405,14 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
 //         registers; the sweep's hand-overs all happened in the band part).
 // The chain of band b is ~0.8 b0 + 2.5 (b1 - b0) + 0.8 (T - b1) tile-times; the
 // cross-band pairs are evaluated twice (ordered), the in-band pairs once.
-// Segmented row blocks (kind 5): a row tile's row block cut into column segments
-// [c0, c1) of tiles, run as separate units in layers (every row tile's first
-// segment, then every second, ...); a segment continues the rows' sums of the one
-// before (F, agent scope; progress counter = the segment's first column tile).  A
-// whole row block is T tiles of one wave; the last ones taken set the launch's
-// tail (N = 8 share of C4: queue drained at 17.9 ms, last block ended at 28.3 ms,
-// profiles/r04/sym_timeline_rows_n8.json), a segment only T / G tiles.
+// Segmented row blocks (kind 5, opt-in GE_FAML_ROWSEG): a row tile's row block cut
+// into column segments [c0, c1) of tiles, run as separate units in layers (every
+// row tile's first segment, then every second, ...); a segment continues the rows'
+// sums of the one before (F, agent scope; progress counter = the segment's first
+// column tile).  A whole row block is T tiles of one wave and the last ones taken
+// set the launch's tail (N = 8 share of C4: queue drained at 17.9 ms, last block
+// ended at 28.3 ms); segments cut the tail to 3.6 ms but not the launch
+// (profiles/r04/sym_timeline_*_n8.json).
 constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3, kUnitRowSeg = 5;
 __host__ __device__ inline int unit_word(int kind, int b0, int b1) {
   return kind | (b0 << 4) | (b1 << 18);
