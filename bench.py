@@ -156,7 +156,10 @@ def pmc_traffic_per_launch(kernel_prefix, workload):
     committed rocprofv3 PMC passes of the same workload (profiles/<round>/pmc_fetch_
     <workload>*.csv and pmc_write_...).  gfx950 correction (MI355X_MICROARCH.md):
     FETCH_SIZE reports half the bytes of a wide coalesced read -> bytes =
-    (2 * FETCH_SIZE + WRITE_SIZE) * 1024."""
+    (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  One "launch" is one pass of the matching
+    kernels: the sum over every matching dispatch divided by the dispatch count of the
+    least frequent matching kernel (the row pass launches its tile kernel twice --
+    segments, tiles -- and its heavy-chain kernel once)."""
     def read(pattern, counter):
         import csv
         for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", pattern)), reverse=True):
@@ -167,7 +170,8 @@ def pmc_traffic_per_launch(kernel_prefix, workload):
                     if row.get("Counter_Name") == counter and name.find(kernel_prefix) >= 0:
                         vals.setdefault(name, []).append(float(row["Counter_Value"]))
             if vals:
-                return sum(sum(v) / len(v) for v in vals.values()), path
+                passes = min(len(v) for v in vals.values())
+                return sum(sum(v) for v in vals.values()) / passes, path
         return None
     f = read(f"pmc_fetch_{workload}*.csv", "FETCH_SIZE")
     w = read(f"pmc_write_{workload}*.csv", "WRITE_SIZE")
