@@ -151,6 +151,15 @@ def baseline_record(value, unit, threads, sample, per_iter):
     return rec
 
 
+def sym_schedule(plan):
+    """The plan's repulsion schedule; None from an older variant library
+    (GE_LIB_PATH A/B runs) that lacks ge_faml_plan_schedule."""
+    try:
+        return plan.schedule()
+    except AttributeError:
+        return None
+
+
 def pmc_traffic_per_launch(kernel_prefix, workload):
     """HBM bytes per launch of the kernels whose names contain kernel_prefix, from the
     committed rocprofv3 PMC passes of the same workload (profiles/<round>/pmc_fetch_
@@ -466,7 +475,7 @@ def run_multilevel(args, rank, world, local, dev):
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
         # this rank's streamed aggregates: plain symmetric sweeps / bands (a shorter
         # dependency chain) / whole row blocks
-        "sym_schedule": pk.schedule(),
+        "sym_schedule": sym_schedule(pk),
         "setup_seconds": {"graph_device": t_gen, "partition_device": t_part,
                           "partition_host": t_part_host, "ptap_device": t_ptap,
                           "plan_build": plan_seconds.get(args.steps),

@@ -1305,6 +1305,28 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     GE_HIP(hipEventRecord(pl->fork, st));
     for (int k = 0; k < 3; ++k) GE_HIP(hipStreamWaitEvent(pl->side[k], pl->fork, 0));
     if (ev) GE_HIP(hipEventRecord(ev[0], st));
+    // resident classes: large on side[1], mid on side[2], small on the context stream
+    auto launch_resident = [&] {
+      if (pl->nl > 0)
+        hipLaunchKernelGGL((faml_resident<D, 256, large_cap(D)>), dim3(pl->nl), dim3(256), 0,
+                           pl->side[1], pl->order.p, pl->beg.p + pl->off_l, pl->pt_ip, pl->pt_ix,
+                           pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p,
+                           pl->Fprev.p, X, iters, c);
+      if (pl->nm > 0)
+        hipLaunchKernelGGL((faml_resident<D, 256, 256>), dim3(pl->nm), dim3(256), 0, pl->side[2],
+                           pl->order.p, pl->beg.p + pl->off_m, pl->pt_ip, pl->pt_ix, pl->pos.p,
+                           pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p,
+                           X, iters, c);
+      if (pl->ns > 0)
+        hipLaunchKernelGGL((faml_resident<D, 64, 64>), dim3(pl->ns), dim3(64), 0, st, pl->order.p,
+                           pl->beg.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
+                           pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X, iters, c);
+    };
+    // GE_FAML_RESIDENT_FIRST=1: the resident classes are queued before the streamed
+    // path (tuning: their overlap with the first repulsion launches)
+    const bool resident_first =
+        std::getenv("GE_FAML_RESIDENT_FIRST") && *std::getenv("GE_FAML_RESIDENT_FIRST") == '1';
+    if (resident_first) launch_resident();
     // streamed path (side[0])
     hipStream_t ss = pl->side[0];
     if (ev) GE_HIP(hipEventRecord(ev[2], ss));
@@ -1401,21 +1423,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                          pl->pt_ip, pl->pt_ix, cur, cA, rA, X);
     }
     if (ev) GE_HIP(hipEventRecord(ev[3], ss));
-    // resident classes: large on side[1], mid on side[2], small on the context stream
-    if (pl->nl > 0)
-      hipLaunchKernelGGL((faml_resident<D, 256, large_cap(D)>), dim3(pl->nl), dim3(256), 0,
-                         pl->side[1], pl->order.p, pl->beg.p + pl->off_l, pl->pt_ip, pl->pt_ix,
-                         pl->pos.p, pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p,
-                         pl->Fprev.p, X, iters, c);
-    if (pl->nm > 0)
-      hipLaunchKernelGGL((faml_resident<D, 256, 256>), dim3(pl->nm), dim3(256), 0, pl->side[2],
-                         pl->order.p, pl->beg.p + pl->off_m, pl->pt_ip, pl->pt_ix, pl->pos.p,
-                         pl->vA, pl->ip, pl->ix, pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X,
-                         iters, c);
-    if (pl->ns > 0)
-      hipLaunchKernelGGL((faml_resident<D, 64, 64>), dim3(pl->ns), dim3(64), 0, st, pl->order.p,
-                         pl->beg.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
-                         pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X, iters, c);
+    if (!resident_first) launch_resident();
     for (int k = 0; k < 3; ++k) GE_HIP(hipEventRecord(pl->join[k], pl->side[k]));
     for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(st, pl->join[k], 0));
     if (ev) GE_HIP(hipEventRecord(ev[1], st));  // resident classes done
