@@ -733,6 +733,7 @@ struct ge_faml_plan {
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
   int banded = 0, rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
+  bool sym_ext = false;  // units of the band / segmented-row kinds: the EXT kernel
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
   std::string stamp_path;
@@ -1176,6 +1177,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     });
     std::vector<int4> h_units;
     for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.word));
+    pl->sym_ext = false;
+    for (const Unit& x : us) {
+      const int kind = x.word & 15, b1 = (x.word >> 18) & kUnitMaxTile;
+      pl->sym_ext = pl->sym_ext || kind == kUnitPre || kind == kUnitRowSeg || (kind == 0 && b1 > 0);
+    }
     pl->nunits = (int)h_units.size();
     pl->ntiles = pb;
     pl->units.alloc(h_units.size());
@@ -1352,8 +1358,10 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
         }
         if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
-          double* H = pl->hand.p;
-          const size_t hs = (size_t)pl->n;
+          // GE_SYM_HAND_F=1: hand-overs through F's records (round-3 layout; A/B only)
+          const bool hand_f = std::getenv("GE_SYM_HAND_F") && *std::getenv("GE_SYM_HAND_F") == '1';
+          double* H = hand_f ? pl->Fscr.p : pl->hand.p;
+          const size_t hs = hand_f ? 0 : (size_t)pl->n;
           int* err = pl->sym_err.p;
           const long long lim = pl->sym_limit;
           if (pl->sym_pair) {
@@ -1376,20 +1384,20 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
             // only with -DGE_SYM_DIAGNOSTICS (scripts/build_variant.sh NAME -DGE_SYM_DIAGNOSTICS), never in the
             // shipped library.
             std::fprintf(stderr, "libge: GE_SYM_NOWAIT diagnostics build: results are invalid\n");
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);
 #endif
           } else if (!pl->stamp_path.empty()) {
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);
           } else {
             sym_repulse_launch(D, pl->sym_blocks, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim);
+                               err, lim, pl->sym_ext);
           }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
@@ -1457,17 +1465,25 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
                         double repel, double* F, double* H, size_t hs, int* prog, int* err,
-                        long long limit) {
+                        long long limit, bool ext) {
   dispatch_dim(dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    if (repel == 1.0)
+    if (ext) {  // band / segmented-row units present
+      if (repel == 1.0)
+        hipLaunchKernelGGL((faml_sym_repulse<D, true, false, false, true>), dim3(blocks),
+                           dim3(kSymT), 0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs,
+                           prog, err, limit, nullptr);
+      else
+        hipLaunchKernelGGL((faml_sym_repulse<D, false, false, false, true>), dim3(blocks),
+                           dim3(kSymT), 0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs,
+                           prog, err, limit, nullptr);
+    } else if (repel == 1.0) {
       hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(blocks), dim3(kSymT), 0, s, nunits,
-                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit,
-                         nullptr);
-    else
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
+    } else {
       hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(blocks), dim3(kSymT), 0, s, nunits,
-                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit,
-                         nullptr);
+                         units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
+    }
   });
   GE_HIP(hipGetLastError());
 }

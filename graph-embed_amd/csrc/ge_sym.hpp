@@ -150,6 +150,13 @@ __device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, c
   }
 }
 
+// Hand-over slot of member c, dimension k: component-major H[k * hs + c], or with
+// hs == 0 record-major H[c * D + k] (H = F, the round-3 layout; GE_SYM_HAND_F=1, A/B)
+template <int D>
+__device__ __forceinline__ double* hand_at(double* H, size_t hs, size_t c, int k) {
+  return hs ? H + k * hs + c : H + c * D + k;
+}
+
 // Column tile t of the sweep has left lane 63: write its sums back, then let the
 // next sweep of the aggregate have it (tprog[t] = done: row tiles < done added).
 // The hand-over buffer H is component-major (H[k * hs + c]): each of the D store
@@ -165,7 +172,7 @@ __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncol
   if (qo < ncols) {
     const double* o = out + (qo & (kSymRing - 1)) * IW;
 #pragma unroll
-    for (int k = 0; k < D; ++k) agent_st(H + k * hs + cbase + qo, o[k]);
+    for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, cbase + qo, k), o[k]);
   }
   // Ordering (no acquire/release: an agent-scope release would write back the whole
   // L2, ~every 64 steps): the sums are agent-scope stores (they bypass the per-XCD
@@ -178,25 +185,41 @@ __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncol
   if (lane == 0) __hip_atomic_store(tprog + t, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The counter as the wave sees it, made wave-uniform so the wait loop below is a
+// scalar loop: a per-lane exit test would make the compiler treat the loop as
+// divergent and hold its counters in VGPRs, which costs the plain kernel the
+// two registers that keep it at 120 (3 waves/SIMD beside the resident kernels).
+__device__ __forceinline__ int seen(const int* flag) {
+  return __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Wait until a column tile's progress counter reaches A.  Bounded: a wait longer
 // than `limit` ticks of the 100 MHz clock, or one another wave already reported
-// in *err, sets *err and gives up for the rest of the launch, so a scheduling bug
-// ends the launch (with wrong sums and an error the host reports) instead of
-// hanging the device.  Returns the ticks spent when STAMP.
+// in *err, makes the wave give up waiting for the rest of the launch (and report
+// in *err as it leaves), so a scheduling bug ends the launch (with wrong sums and
+// an error the host reports) instead of hanging the device.  The store is kept out
+// of the loop: inside it, at the kernel's register peak, it cost two VGPRs.
+// Returns the ticks spent when STAMP.
+// system scope: err may be pinned host memory (single-level plans)
+__device__ __forceinline__ void report_give_up(bool give_up, int lane, int* err) {
+  if (give_up && lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool STAMP>
 __device__ __forceinline__ long long handover_wait(const int* flag, int A, int* err,
                                                    long long limit, bool& give_up) {
   if (give_up) return 0;
-  if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A) return 0;
+  if (seen(flag) >= A) return 0;
   const long long t0 = rt_now();
   for (int k = 1;; ++k) {
     __builtin_amdgcn_s_sleep(1);
-    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= A) break;
+    if (seen(flag) >= A) break;
     if ((k & 255) == 0 &&
-        (rt_now() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
-      // system scope: err may be pinned host memory (single-level plans)
-      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      give_up = true;
+        (rt_now() - t0 > limit ||
+         __builtin_amdgcn_readfirstlane(
+             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)))) {
+      give_up = true;  // the kernel reports it on its way out (report_give_up)
       break;
     }
   }
@@ -330,7 +353,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
-      ic[k] = (cv && A > 0) ? agent_ld(H + k * hs + cbase + qc) : 0.0;
+      ic[k] = (cv && A > 0) ? agent_ld(hand_at<D>(H, hs, cbase + qc, k)) : 0.0;
     }
     if (cv) dc = DP[cbase + qc];
     const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
@@ -425,7 +448,16 @@ constexpr int kUnitMaxTile = (1 << 14) - 1;  // band tile indices are 14-bit fie
 // waits only on units before it in the queue.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
 // (diagnostics, wrong results): no sweep waits for its hand-overs.
-template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
+// EXT: the band and segmented-row unit kinds (kinds 3 and 5, band ends of sweeps).
+// The plain kernel (sweeps and whole row blocks only) stays at <= 120 VGPRs: three
+// of its waves per SIMD (the plan's three blocks per CU) then leave 152 of the 512
+// registers, room for one wave of the resident classes' kernels (143 VGPRs) on the
+// other streams.  With the extra kinds compiled in (or the give-up store inside the
+// wait loop) it took 122-128, the resident kernels were locked out until the
+// repulsion launches ended and ran during the attraction passes instead (C4: 4.44
+// against 3.52 ms per pass, 140.4 against 137.0-137.3 ms per step, the round-3
+// library 138.7-138.9 on the same box; profiles/r04/ab_rows_r03.log).
+template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false, bool EXT = false>
 __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
@@ -443,7 +475,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
   double* ini = sini[threadIdx.x >> 6];
   double* out = sout[threadIdx.x >> 6];
   const bool repel_ok = REPEL_ONE || weight_ok(repel);
-  bool give_up = false;  // a hand-over wait timed out (err is set)
+  bool give_up = false;  // a hand-over wait timed out (err is set on exit)
   for (;;) {
     int qi = 0;
     if (lane == 0) qi = atomicAdd(queue, 1);
@@ -463,7 +495,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
-    } else if (kind == kUnitRowSeg) {  // columns [64 b0, 64 b1) of row tile A's row block
+    } else if (EXT && kind == kUnitRowSeg) {  // columns [64 b0, 64 b1) of row tile A's row block
       const bool first = b0 == 0, last = 64 * b1 >= s;
       double acc[D];
       if (!first) {  // the segment before has stored the rows' sums
@@ -491,7 +523,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
         if (lane == 0)
           __hip_atomic_store(prog + u.z + A, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    } else if (kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
+    } else if (EXT && kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
       __builtin_amdgcn_s_setprio(3);
       double acc[D];
       rows_range<D, REPEL_ONE>(lane, base, s, A, 0, 64 * b0, true, X, DP, repel, repel_ok, rec,
@@ -499,7 +531,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       __builtin_amdgcn_s_setprio(0);
       if (64 * A + lane < s) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) agent_st(H + k * hs + rb + lane, acc[k]);
+        for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, rb + lane, k), acc[k]);
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       __builtin_amdgcn_s_waitcnt(0);
@@ -509,7 +541,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     } else {
       // a sweep; in a band that is not the aggregate's last it stops at the band's
       // end and the same wave continues its rows past the band (post)
-      const bool banded = b1 > 0 && 64 * b1 < s;
+      const bool banded = EXT && b1 > 0 && 64 * b1 < s;
       double racc[D];
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, ini,
@@ -527,6 +559,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
   }
+  report_give_up(give_up, lane, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -768,6 +801,7 @@ faml_sym_pair(int nunits, const int4* __restrict__ units, int* __restrict__ queu
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();
   }
+  report_give_up(give_up, lane, err);
 }
 
 }  // namespace ge

@@ -38,7 +38,8 @@ def main():
     a = ap.parse_args()
     dim = 3
     t0 = time.perf_counter()
-    A = ge.rmat_csr(a.n, a.draws, seed=a.seed)
+    ctx = ge.Context(0)
+    A = ctx.rmat_csr(a.n, a.draws, seed=a.seed)  # device generator (= the host arrays)
     n, nnz = len(A[0]) - 1, int(A[0][-1])
     print(f"R-MAT n={n} nnz={nnz} max deg={int(np.diff(A[0]).max())} "
           f"generated in {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
@@ -54,7 +55,6 @@ def main():
     frep = (torch.rand(n, dim, dtype=torch.float64, device=dev, generator=g) * 2 - 1) * \
         ((deg + 1) * 1e6)[:, None]
     y = torch.empty_like(x)
-    ctx = ge.Context(0)
     t0 = time.perf_counter()
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), dim, 0, n)
     print(f"plan {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
