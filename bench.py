@@ -554,7 +554,11 @@ def run_single_level(args, rank, world, local, dev):
     rep_tflops = FLOPS_PER_PAIR * pairs / (rep_ms * 1e-3) / 1e12 if rep_ms > 0 else 0.0
     attr_bytes = 12 * nnz * rows / n + 52 * rows + 4  # SURVEY 8(d) B_attr, this rank's rows
     att_gbs = attr_bytes / (att_ms * 1e-3) / 1e9 if att_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic_per_launch("fa_repulse", "c2")
+    # the plan's repulsion kernel (ge_fa.hip plan_init): symmetric sweeps for a STRICT
+    # plan over every row (one rank), the ordered-pair kernel on a row shard or FAST
+    sym = (args.mode == "strict" and world == 1 and os.environ.get("GE_FA_SYM", "") != "0")
+    rep_kernel = "faml_sym_repulse" if sym else "fa_repulse_%s" % args.mode
+    traffic, traffic_src = pmc_traffic_per_launch(rep_kernel, "c2")
     att_traffic, att_src = pmc_traffic_per_launch("FaRows", "c2")
     result = {
         "metric": METRIC, "value": its, "unit": "iterations/s", "n_gpus": world,
@@ -569,12 +573,17 @@ def run_single_level(args, rank, world, local, dev):
         "edges_per_s": nnz * its,
         "pair_interactions_per_s": n * (n - 1) * its,
         "finite": finite,
-        "roofline": {"kernel": "fa_repulse_%s (all-pairs repulsion, fp64)" % args.mode,
+        "roofline": {"kernel": rep_kernel + (" (single-level symmetric sweeps: one aggregate of all"
+                                             " n rows, fp64)" if sym else
+                                             " (all-pairs repulsion, fp64)"),
                      "bound": "valu", "pipe": "fp64 VALU; priced against the FP64 vector peak "
                                               "(78.6 TFLOP/s, spec)",
                      "achieved": rep_tflops, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": rep_tflops / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_source": traffic_src, "flops_per_launch": FLOPS_PER_PAIR * pairs,
+                     "flops_per_unit": "26 per ordered pair (7d+5, d=3)" + (
+                         "; the symmetric kernel evaluates each unordered pair once and credits"
+                         " both ordered pairs" if sym else ""),
                      "avg_launch_ms": rep_ms, "launches": launches},
         "roofline_attraction": {"kernel": "tile_rows_kernel<FaRows> + classed_rows_kernel<FaRows>"
                                           " (CSR attraction + gravity + update; fork to join)",
