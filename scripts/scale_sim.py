@@ -2,7 +2,17 @@
 every rank's share (ge_assign_aggregates, the deal bench.py uses) runs as its own
 subset plan, one after another, and its kernel time per iteration is measured.
 max over ranks approximates the N-GPU step (the member all-gather, once per call,
-is left out); efficiency = t(1) / (N * max).  Prints one JSON line per N."""
+is left out); efficiency = t(1) / (N * max).  Prints one JSON line per N.
+
+SPLIT_MIN=k (SURVEY.md 8(e) split): aggregates of >= k members are split by row
+tiles over all N ranks (ge_assign_aggregates_split), each rank's shard plan runs its
+row tiles of them as row blocks and exchanges the split rows after every iteration.
+The exchange goes through a local transport that copies the rank's own block into
+every slot (finite coordinates, host round trip), so the per-iteration wall time
+includes a PCIe copy RCCL would not make; the kernel times (repulse_ms, rows_ms)
+are unaffected, and the exchange is priced from its bytes at XGMI_GBS (bus
+bandwidth of an RCCL all-gather, default 300 GB/s)."""
+import ctypes
 import json
 import os
 import sys
@@ -14,6 +24,25 @@ import torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "graph-embed_amd", "py"))
 import ge_amd as ge  # noqa: E402
+
+
+def local_comm(ctx, N, r):
+    """A ge_comm of N ranks whose all-gather copies this rank's block into every slot."""
+    c = ge.Comm.__new__(ge.Comm)
+    c.ctx, c.nranks, c.rank = ctx, N, r
+
+    def cb(user, send, recv, nbytes):
+        for k in range(N):
+            ctypes.memmove(recv + k * nbytes, send, nbytes)
+        return 0
+    c._cb = ge._ALLGATHER_FN(cb)
+    c._tp = ge._Transport(None, c._cb)
+    h = ctypes.c_void_p()
+    ge._check(ge.lib().ge_comm_create_transport(ctx.h, N, r, ctypes.cast(ctypes.byref(c._tp),
+                                                                         ctypes.c_void_p),
+                                                ctypes.byref(h)))
+    c.h = h
+    return c
 
 
 def main():
@@ -36,8 +65,14 @@ def main():
         np.savez(os.environ["SAVE_LEVEL"], pt_ip=PT[0], entries=ent)
     t1 = None
     for N in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
-        owner = ge.assign_aggregates(PT, L[0], N)
-        times, reps, scheds = [], [], []
+        split_min = int(os.environ.get("SPLIT_MIN", "0"))
+        if split_min > 0 and N > 1:
+            owner = ge.assign_aggregates_split(PT, L[0], N, split_min)
+        else:
+            owner = ge.assign_aggregates(PT, L[0], N)
+        split = np.flatnonzero(owner < 0).astype(np.int32)
+        split_rows = int(sum(PT[0][a + 1] - PT[0][a] for a in split))
+        times, reps, rows_ms, scheds = [], [], [], []
         for r in range(N):
             mine = np.flatnonzero(owner == r).astype(np.int32)
             # STAMP_N=N: the per-unit timeline of rank 0's last launch (GE_SYM_STAMPS,
@@ -46,9 +81,11 @@ def main():
                 os.environ["GE_SYM_STAMPS"] = os.path.join(REPO, "gpurun_out", f"stamps_N{N}.bin")
             else:
                 os.environ.pop("GE_SYM_STAMPS", None)
+            comm = local_comm(ctx, N, r) if len(split) else None
             p = ge.FamlPlan(ctx, n0, d["ip"].data_ptr(), d["ix"].data_ptr(), d["dx"].data_ptr(),
                             PT[0], d["pip"].data_ptr(), d["pix"].data_ptr(), d["vA"].data_ptr(),
-                            dim, iterations=iters, aggs=mine if N > 1 else None)
+                            dim, iterations=iters, aggs=mine if N > 1 else None,
+                            split=split if comm else None, comm=comm)
             p.run(d["cA"].data_ptr(), d["rA"].data_ptr(), d["init"].data_ptr(), X.data_ptr())
             ctx.sync()
             p.set_profiling(True)
@@ -58,12 +95,23 @@ def main():
             times.append((time.perf_counter() - t0) / iters * 1e3)
             rep_ms, _, _ = p.repulse_ms()
             reps.append(rep_ms)
+            rows_ms.append(p.rows_ms()[0])
             scheds.append(p.schedule())
             p.close()
+            if comm:
+                comm.close()
         t1 = t1 or times[0]
-        print(json.dumps({"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times), "repulse_ms_by_rank": reps,
-                          "schedule_by_rank": scheds,
-                          "efficiency": t1 / (N * max(times))}), flush=True)
+        rec = {"N": N, "ms_per_iteration_by_rank": times, "max_ms": max(times),
+               "repulse_ms_by_rank": reps, "rows_ms_by_rank": rows_ms,
+               "schedule_by_rank": scheds, "efficiency": t1 / (N * max(times))}
+        if len(split):
+            gbs = float(os.environ.get("XGMI_GBS", "300"))
+            xbytes = split_rows * dim * 8
+            rec.update(split_aggregates=int(len(split)), split_rows=split_rows,
+                       exchange_bytes_per_iteration=xbytes,
+                       exchange_ms_priced=xbytes * (N - 1) / N / (gbs * 1e9) * 1e3,
+                       note="ms_per_iteration includes a host round trip of the exchange")
+        print(json.dumps(rec), flush=True)
     ctx.close()
 
 
