@@ -15,6 +15,10 @@
 #                    per-block limits) over bench W (3 steps), dispatches matching RE
 #                    (default: the multilevel / single-level repulsion and row kernels)
 #                                                            -> pmc_<CTRS>_W.csv (+ summary)
+#   c5[:ARGS]        scripts/c5_attraction.py [ARGS]  (configs[4] attraction pass)
+#                                                            -> c5_attraction.json
+#   pmc5:CTRS        one --pmc pass over c5_attraction.py (2 passes + 1 warmup),
+#                    attraction kernels only             -> pmc_<CTRS>_c5.csv (+ summary)
 #   py:SCRIPT[:ARGS] python -u SCRIPT [ARGS, commas = spaces] -> SCRIPT-name.log
 #   env:K=V          export K=V for the following steps
 set -o pipefail
@@ -63,6 +67,19 @@ for step in "$@"; do
       rm -rf $OUT/pmc_$name
       python3 scripts/pmc_summary.py $OUT/pmc_${name}_$a.csv "" > $OUT/pmc_${name}_$a.txt 2>&1
       cat $OUT/pmc_${name}_$a.txt ;;
+    c5)
+      timeout -k 10 600 python -u scripts/c5_attraction.py ${a//,/ } > $OUT/c5_attraction.json \
+        2> $OUT/c5_attraction.err || fail "$step" $? $OUT/c5_attraction.err
+      cat $OUT/c5_attraction.json ;;
+    pmc5)
+      name=${a//,/_}
+      timeout -s KILL 600 rocprofv3 --pmc ${a//,/ } --kernel-include-regex "rows_kernel|heavy_" \
+        --output-format csv -d $OUT/pmc5_$name -o p -- python3 scripts/c5_attraction.py --steps 2 \
+        --warmup 1 > $OUT/pmc_${name}_c5.log 2>&1 || fail "$step" $? $OUT/pmc_${name}_c5.log
+      cp "$(find $OUT/pmc5_$name -name '*counter_collection.csv' | head -1)" $OUT/pmc_${name}_c5.csv
+      rm -rf $OUT/pmc5_$name
+      python3 scripts/pmc_summary.py $OUT/pmc_${name}_c5.csv "" > $OUT/pmc_${name}_c5.txt 2>&1
+      cat $OUT/pmc_${name}_c5.txt ;;
     py)
       log=$OUT/$(basename $a .py).log
       timeout -k 10 1200 python -u $a ${b//,/ } > $log 2>&1 || fail "$step" $? $log
