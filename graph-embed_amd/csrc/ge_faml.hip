@@ -1356,6 +1356,12 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_rev += 2;
           GE_HIP(hipEventRecord(re[0], ss));
         }
+        const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
+                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
+        // the heavy member rows' segment terms need only `cur`: queued beside the
+        // repulsion launch (ge_rows.hpp launch_rows_early)
+        const bool rows_early =
+            pl->nrows > 0 && launch_rows_early<D>(pl->ecls, fr, ss, pl->rstreams);
         if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
           // GE_SYM_HAND_F=1: hand-overs through F's records (round-3 layout; A/B only)
@@ -1416,11 +1422,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_aev += 2;
           GE_HIP(hipEventRecord(ae[0], ss));
         }
-        if (pl->nrows > 0) {
-          const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
-                               cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
-          launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
-        }
+        if (pl->nrows > 0) launch_rows<D>(pl->ecls, fr, ss, pl->rstreams, rows_early);
         if (ae) GE_HIP(hipEventRecord(ae[1], ss));
         if (pl->xwidth > 0)  // every rank's rows of the split aggregates, for the next step
           exchange_rows(pl->comm, ss, D, pl->xrows.p, pl->xcounts.p, pl->xfirst.p,

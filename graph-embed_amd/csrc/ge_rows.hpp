@@ -730,20 +730,47 @@ struct RowStreams {
       (void)hipStreamDestroy(side);
     }
     if (fork) (void)hipEventDestroy(fork);
+    if (mid) (void)hipEventDestroy(mid);
     if (join) (void)hipEventDestroy(join);
   }
   void ensure() {
     if (side) return;
     GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     GE_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    GE_HIP(hipEventCreateWithFlags(&mid, hipEventDisableTiming));
     GE_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   }
+  hipEvent_t mid = nullptr;  // launch_rows after launch_rows_early: the sums are ready
 };
 
-// All rows of `rc` on stream s (the heavy ones on rs.side when there are tiles;
-// s waits for them before returning to the caller's next work).
+// kSegStore with tiles: the heavy rows' segment terms depend on the coordinates
+// only, not on the accumulators' start values (the repulsion sums).  Called before
+// the launch that writes those sums (the streamed repulsion), this queues the
+// segments on rs.side at once, so they run beside that launch; the matching
+// launch_rows(..., early = true) then queues only the chains and the tiles.
+// Returns whether it did.  Opt-in (GE_ROWS_EARLY=1): bit-exact, and the C4 pass
+// fell from 3.54 to 2.2-2.4 ms, but the repulsion launch beside it rose from 136.3
+// to 141-142 ms (140.6 against 144-145 ms per step, profiles/r04/ab_rows_early.log).
 template <int D, class P>
-inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
+inline bool launch_rows_early(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
+  if (!(rc.nseg > 0 && rc.seg_mode == kSegStore && rc.ntiles > 0) || std::getenv("GE_ROWS_SERIAL"))
+    return false;
+  const char* e = std::getenv("GE_ROWS_EARLY");
+  if (!(e && *e == '1')) return false;
+  rs.ensure();
+  GE_HIP(hipEventRecord(rs.fork, s));
+  GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+  hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
+                     rc.ntiles);
+  return true;
+}
+
+// All rows of `rc` on stream s (the heavy ones on rs.side when there are tiles;
+// s waits for them before returning to the caller's next work).  early: the
+// segments were queued by launch_rows_early with the same arguments.
+template <int D, class P>
+inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs,
+                        bool early = false) {
   const int tgrid = rc.ntiles + rc.nseg;
   if (rc.nseg > 0 && rc.seg_mode == kSegStore && rc.ntiles > 0 &&
       !std::getenv("GE_ROWS_SERIAL")) {
@@ -751,10 +778,15 @@ inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStre
     // dependent add per term) is independent of the tiles: segments + chains on the
     // side stream, beside the tiles (C4: 2.16 + 1.43 ms one after the other)
     rs.ensure();
-    GE_HIP(hipEventRecord(rs.fork, s));
-    GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
-                       rc.ntiles);
+    if (early) {  // the chains also wait for the sums written on s
+      GE_HIP(hipEventRecord(rs.mid, s));
+      GE_HIP(hipStreamWaitEvent(rs.side, rs.mid, 0));
+    } else {
+      GE_HIP(hipEventRecord(rs.fork, s));
+      GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+      hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
+                         rc.ntiles);
+    }
     hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy), dim3(64), 0, rs.side, rc, p);
     hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles), dim3(kRowT), 0, s, rc, p, 0);
     GE_HIP(hipEventRecord(rs.join, rs.side));

@@ -533,6 +533,29 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, re
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("sym,dim", [("1", 3), ("0", 3), ("1", 2), ("1", 4)])
+def test_faml_rows_early_segments(ctx, oracle, monkeypatch, sym, dim):
+    """GE_ROWS_EARLY=1 (ge_rows.hpp launch_rows_early): the heavy member rows'
+    segment terms queued beside the streamed repulsion launch, their chains and the
+    tiles after it -- symmetric sweeps and the ordered-pair kernel, hub rows longer
+    than one segment."""
+    monkeypatch.setenv("GE_ROWS_EARLY", "1")
+    monkeypatch.setenv("GE_ROWS_TILES", "1")
+    monkeypatch.setenv("GE_FAML_SYM", sym)
+    sizes = [3000, 700, 2203, 90, 1]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=9), [(3, 2600), (40, 5000)], seed=dim)
+    assert np.diff(A[0]).max() > 4096
+    PT = _block_partition(n, sizes, seed=4)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=19)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=19)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("chain,dim,repel", [
     ("0", 3, 1.0), ("0", 3, 1.5), ("0", 3, 2.0 ** 70), ("1e9", 3, 1.0), ("", 3, 1.0),
     ("0", 2, 1.0), ("0", 4, 0.75), ("1e9", 4, 1.0)])
