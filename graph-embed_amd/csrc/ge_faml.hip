@@ -1433,6 +1433,14 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                          pl->pt_ip, pl->pt_ix, cur, cA, rA, X);
     }
     if (ev) GE_HIP(hipEventRecord(ev[3], ss));
+    // GE_FAML_RESIDENT_SERIAL=1 (tuning): the resident classes only after the streamed
+    // path, not beside it
+    if (std::getenv("GE_FAML_RESIDENT_SERIAL") && *std::getenv("GE_FAML_RESIDENT_SERIAL") == '1' &&
+        !resident_first) {
+      GE_HIP(hipEventRecord(pl->join[0], ss));
+      for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(pl->side[k], pl->join[0], 0));
+      GE_HIP(hipStreamWaitEvent(st, pl->join[0], 0));
+    }
     if (!resident_first) launch_resident();
     for (int k = 0; k < 3; ++k) GE_HIP(hipEventRecord(pl->join[k], pl->side[k]));
     for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(st, pl->join[k], 0));
