@@ -115,6 +115,67 @@ def test_c4_level0_sampled_aggregates(ctx, oracle, heartbeat):
     assert np.isfinite(got).all()
 
 
+def test_c4_level0_schedules_agree_at_embed_horizon(ctx, monkeypatch, heartbeat):
+    """C4 level 0 over the embed's 100 iterations (src/embed.cpp:793): the streamed
+    aggregates (98 at C4, up to 41 930 members) as symmetric sweeps (the default), as
+    ordered row blocks (GE_FAML_SYM_CHAIN=1e9) and through the ordered-pair kernel
+    (GE_FAML_SYM=0) give the same bits.  Each schedule is pinned to the oracle on
+    small levels (test_gpu_parity.py) and at C4 for 2 iterations above; the oracle
+    would need hours for 100 iterations of these aggregates, so the long horizon is
+    checked as agreement of three independent schedules (a hand-over or queue-order
+    fault shows as a difference)."""
+    import time
+    t0 = time.perf_counter()
+    L = ge.largest_component(ge.rmat_csr(10_000_000, 80_000_000, seed=12345))
+    PT = ctx.partition(L, 0.125)[0]
+    _progress(t0, "C4 device partition")
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = ge.uniform_stream(7, m * 3).reshape(m, 3)
+    rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
+    runs = {}
+    for name, env in (("sweeps", {}), ("row_blocks", {"GE_FAML_SYM_CHAIN": "1e9"}),
+                      ("ordered_pairs", {"GE_FAML_SYM": "0"})):
+        for k in ("GE_FAML_SYM_CHAIN", "GE_FAML_SYM"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with heartbeat(f"C4 level 0, 100 iterations, {name}"):
+            runs[name] = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=100, seed=5)
+        _progress(t0, f"C4 {name} done")
+    assert np.isfinite(runs["sweeps"]).all()
+    assert np.array_equal(runs["sweeps"], runs["row_blocks"])
+    assert np.array_equal(runs["sweeps"], runs["ordered_pairs"])
+
+
+def test_c4_embed_end_to_end_schedules_agree(ctx, monkeypatch, heartbeat):
+    """The whole C4 embed (examples/embed.cpp: 4 levels of the device partition,
+    P^T A P, the coarsest level's 1e5 iterations, radius steps, 100 multilevel
+    iterations per level) with the shipped kernels -- symmetric sweeps, packed
+    coarsest rows -- and with the independent ones -- the ordered-pair multilevel
+    kernel (GE_FAML_SYM=0), one wave per coarsest row (GE_FA_PACKED=0): the same
+    bits end to end (bench.py checks only finiteness)."""
+    import time
+    t0 = time.perf_counter()
+    L = ge.largest_component(ge.rmat_csr(10_000_000, 80_000_000, seed=12345))
+    hier = ctx.partition(L, 0.125)[:4]
+    As = [L]
+    for PT in hier:
+        As.append(ctx.ptap(As[-1], PT))
+    _progress(t0, "C4 hierarchy and P^T A P")
+    runs = {}
+    for name, env in (("shipped", {}), ("independent", {"GE_FAML_SYM": "0", "GE_FA_PACKED": "0"})):
+        for k in ("GE_FAML_SYM", "GE_FA_PACKED"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with heartbeat(f"C4 embed, {name} kernels"):
+            runs[name] = ctx.embed(As, hier, 3, seed=12345)
+        _progress(t0, f"C4 embed {name} done")
+    assert np.isfinite(runs["shipped"]).all()
+    assert np.array_equal(runs["shipped"], runs["independent"])
+
+
 def _coarse_rows_numpy(L, PT, vA, rows):
     """Rows of P_T A P for the coarse ids `rows`, straight from the definition (entry
     (a, b) = sum of a_ij over i in a, j in b): exact, since the
