@@ -735,7 +735,16 @@ struct RowStreams {
   }
   void ensure() {
     if (side) return;
-    GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    // GE_ROWS_SIDE_PRIO=1: the side stream (heavy segments + chains, the pass's
+    // longer branch) at the device's highest stream priority (tuning)
+    const char* e = std::getenv("GE_ROWS_SIDE_PRIO");
+    if (e && *e == '1') {
+      int least = 0, greatest = 0;
+      GE_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      GE_HIP(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, greatest));
+    } else {
+      GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    }
     GE_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
     GE_HIP(hipEventCreateWithFlags(&mid, hipEventDisableTiming));
     GE_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
