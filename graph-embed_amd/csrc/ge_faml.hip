@@ -1109,7 +1109,18 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     if (const char* e = std::getenv("GE_FAML_SYM_EST")) est_k = std::atof(e);
     const bool est_prop = !(std::getenv("GE_FAML_SYM_PROP") && *std::getenv("GE_FAML_SYM_PROP") == '0');
     const int Tmax = big.empty() ? 1 : *std::max_element(T.begin(), T.end());
-    auto scale_of = [&](int Tb) { return est_prop ? (double)Tmax / Tb : 1.0; };
+    // Big aggregates a little ahead: positions also scaled by 1 - g T / Tmax (g = 0.3),
+    // so the largest chains finish before the queue's end and the small aggregates'
+    // short chains fill it (C4, one box, 3 rounds interleaved: 136.2-136.4 against
+    // 136.9-137.3 ms per step; g = 0.15 136.5-136.7, 0.5 and 0.7 slower;
+    // profiles/r04/ab_big_first.log).  Positions stay increasing in A for g < 1, so
+    // every unit still waits only on units before it.  GE_FAML_SYM_BIGFIRST=g overrides.
+    double big_first = 0.3;
+    if (const char* e = std::getenv("GE_FAML_SYM_BIGFIRST"))
+      big_first = std::min(0.9, std::max(0.0, std::atof(e)));
+    auto scale_of = [&](int Tb) {
+      return (est_prop ? (double)Tmax / Tb : 1.0) * (1.0 - big_first * Tb / Tmax);
+    };
     std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b) {
       const int K = mode_of(b);
