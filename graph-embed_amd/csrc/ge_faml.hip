@@ -31,7 +31,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <numeric>
+#include <queue>
 #include <string>
 #include <vector>
 
@@ -505,12 +507,51 @@ __global__ void edge_code_kernel(int nrows, const int* __restrict__ rows,
   }
 }
 
+// The static part of every external pull of the streamed members (one wave per
+// row): pull[e] = ((cA[b] - cA[a]) / dis_ab) * 100 for k < D (include/forceatlas.hpp
+// :453-465: direction * Fao_ij, evaluated left to right before the division by
+// mag), and pull[e][D] = 1.0 when cA[a] and cA[b] are in the shared-reciprocal
+// domain (the condition under which pull_edge used div_by).  Computed with `/`,
+// which equals div_by in that domain, so FamlRows::term gets pull_edge's bits.
+template <int D>
+__global__ void __launch_bounds__(256)
+pull_precompute_kernel(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ix,
+                       const int* __restrict__ ip, const int* __restrict__ ecode,
+                       const int* __restrict__ vA, const double* __restrict__ cA,
+                       double* __restrict__ pull) {
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= nrows) return;
+  const int v = pt_ix[rows[q]];
+  const double* ca = cA + (size_t)vA[v] * D;
+  const bool ca_ok = all_coord_ok<D>(ca);
+  for (int e = ip[v] + lane; e < ip[v + 1]; e += 64) {
+    const int code = ecode[e];
+    if (code >= 0) continue;
+    const double* cb = cA + (size_t)(-code - 1) * D;
+    double t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) t[k] = cb[k] - ca[k];
+    double qd = t[0] * t[0];
+#pragma unroll
+    for (int k = 1; k < D; ++k) qd = qd + t[k] * t[k];
+    const double dis = clamp_eps(sqrt(qd));
+    double* pu = pull + (size_t)e * (D + 1);
+#pragma unroll
+    for (int k = 0; k < D; ++k) pu[k] = (t[k] / dis) * 100.0;
+    pu[D] = (ca_ok && all_coord_ok<D>(cb)) ? 1.0 : 0.0;
+  }
+}
+
 template <int D>
 struct FamlRows {
   const int *pt_ip, *pt_ix, *ecode, *ip, *vA;
   const double *dx, *cA, *Xc, *DP, *Fscr;
   double *Xn, *Fprev;
   MlConst c;
+  // per CSR entry e of a streamed member, D + 1 doubles (pull_precompute_kernel):
+  // the external pull's ((cA[b] - cA[a]) / dis) * 100, static while cA is, and 1.0
+  // when cA[a] and cA[b] are in the shared-reciprocal domain; nullptr: gathered
+  const double* pull = nullptr;
   struct State {
     int cpos, a, li, e0, e1;
     double xi[D], acc[D], fprev[D], dip1, mag;
@@ -542,6 +583,23 @@ struct FamlRows {
   }
   __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
     const int code = ecode[e];
+    if (pull && code < 0) {
+      // external pull (:453-465) with its static part precomputed: the term is
+      // (direction * 100) / mag, and only the division by the row's mag is left --
+      // the same division, on the same operands, as pull_edge's
+      const double* pu = pull + (size_t)e * (D + 1);
+      double u[D];
+#pragma unroll
+      for (int k = 0; k < D; ++k) u[k] = pu[k];
+      if (s.row_ok && pu[D] != 0.0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = div_by(u[k], s.mag, s.rmag);
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) t[k] = u[k] / s.mag;
+      }
+      return;
+    }
     // the neighbour's (or its aggregate's) coordinates into registers before
     // the branch, so a thread's gathers issue together
     const double* src = code >= 0 ? Xc + (size_t)code * D : cA + (size_t)(-code - 1) * D;
@@ -719,6 +777,7 @@ struct ge_faml_plan {
   int ns = 0, nm = 0, nl = 0, nhuge = 0;
   size_t off_m = 0, off_l = 0;
   ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge, ecode;
+  ge::DevBuf<double> pull;  // FamlRows::pull (allocated when it fits, GE_FAML_PULL=0: off)
   ge::RowClasses ecls;
   ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
@@ -733,6 +792,7 @@ struct ge_faml_plan {
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
   int banded = 0, rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
+  int tail_split = 0;  // row blocks cut into a head and a tail segment (faml_plan_build)
   bool sym_ext = false;  // units of the band / segmented-row kinds: the EXT kernel
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
@@ -870,6 +930,11 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::vector<int> hdeg;
     classify_rows(rows, deg, erows, pl->ecls, kSegStore, &hdeg);
     pl->ecode.alloc(std::max(h_ip[pl->n], 1));
+    {  // precomputed external pulls: (D + 1) doubles per CSR entry of the level
+      const double bytes = (double)h_ip[pl->n] * (pl->dim + 1) * sizeof(double);
+      const char* e = std::getenv("GE_FAML_PULL");
+      if (!(e && *e == '0') && bytes <= 8e9) pl->pull.alloc((size_t)h_ip[pl->n] * (pl->dim + 1));
+    }
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
     pl->ecls.bind(pl->erows.p);
@@ -1179,6 +1244,100 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       for (int A = t0; A < t1; ++A)
         rows_units.push_back({a, A, 0, Ta, unit_word(kUnitRows, 0, 0), -1.0});
     }
+    // Tail split (round 5).  A share of a multi-GPU run that is all row blocks holds
+    // ~2.1 (N = 8) or ~4.2 (N = 4) row blocks of 500-656 tiles per wave, so the
+    // longest-first queue ends with a last round on a few hundred waves: at N = 8 the
+    // queue drained at 17.9 ms and the last block ended at 28.3 ms
+    // (profiles/r04/sym_timeline_rows_n8.json).  A row block's rows add their partners
+    // in order, so it cannot be cut into parallel pieces, but it can be cut in two
+    // consecutive column segments run at different times (McNaughton's wrap-around):
+    // the head (columns [0, 64 h)) at the front of the queue, the tail (the rest,
+    // continuing the rows' sums from F) at its end, where the smaller pieces fill the
+    // waves evenly.  The head is long done when its tail is taken.  Which blocks are
+    // cut (the k smallest) and where (h = f T) is chosen by list-scheduling the queue
+    // on the plan's waves.  Bit-exact (test_faml_tail_split_row_blocks), but measured
+    // no faster (N = 8 shares 26.6-28.0 against 27.0-27.3 ms per launch,
+    // profiles/r05/scale_sim_c4_tailsplit.log): the share is bound by the row blocks'
+    // instruction stream, not by the queue's last round -- opt-in GE_FAML_TAILSPLIT=1
+    // (GE_FAML_TAILSPLIT_K / _F force the cut for tests).
+    pl->tail_split = 0;
+    {
+      const char* e = std::getenv("GE_FAML_TAILSPLIT");
+      const bool on = (e && *e == '1') || std::getenv("GE_FAML_TAILSPLIT_K");
+      bool all_rows = on && !rows_units.empty() && std::getenv("GE_FAML_ROWSEG") == nullptr;
+      all_rows = all_rows && us.empty();  // sweeps present: not a rows-only share
+      for (const Unit& x : rows_units) all_rows = all_rows && (x.word & 15) == kUnitRows && x.T >= 4;
+      if (all_rows) {
+        std::stable_sort(rows_units.begin(), rows_units.end(),
+                         [](const Unit& x, const Unit& y) { return x.T > y.T; });
+        const int m = std::max(1, (int)waves);
+        const size_t nu = rows_units.size();
+        double seg_cost = 1.0;  // tile-times per extra segment (F hand-over, restart)
+        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_COST")) seg_cost = std::atof(s);
+        // list schedule of the queue: heads of the k last blocks, whole blocks, tails
+        auto simulate = [&](size_t k, double f) {
+          std::priority_queue<double, std::vector<double>, std::greater<double>> freeq;
+          for (int w = 0; w < m; ++w) freeq.push(0.0);
+          std::vector<double> head_end(nu, 0.0);
+          auto take = [&](double dur, double ready) {
+            const double t0 = std::max(freeq.top(), ready);
+            freeq.pop();
+            freeq.push(t0 + dur);
+            return t0 + dur;
+          };
+          double span = 0.0;
+          for (size_t i = nu - k; i < nu; ++i) {
+            const int T = rows_units[i].T, h = std::min(T - 1, std::max(1, (int)std::lround(f * T)));
+            head_end[i] = take(h + seg_cost, 0.0);
+          }
+          for (size_t i = 0; i < nu - k; ++i) span = std::max(span, take(rows_units[i].T, 0.0));
+          for (size_t i = nu - k; i < nu; ++i) {
+            const int T = rows_units[i].T, h = std::min(T - 1, std::max(1, (int)std::lround(f * T)));
+            span = std::max(span, take(T - h + seg_cost, head_end[i]));
+          }
+          return span;
+        };
+        double best_span = simulate(0, 0.5), best_f = 0.5;
+        size_t best_k = 0;
+        const size_t step = std::max<size_t>(1, nu / 128);
+        for (double f : {0.5, 0.6, 0.7, 0.8, 0.9})
+          for (size_t k = step; k <= nu; k += step) {
+            const double sp = simulate(k, f);
+            if (sp < best_span * 0.999) {
+              best_span = sp;
+              best_k = k;
+              best_f = f;
+            }
+          }
+        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_K")) best_k = std::min(nu, (size_t)std::atol(s));
+        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_F")) best_f = std::atof(s);
+        if (best_k > 0 && std::getenv("GE_FAML_PLAN_DEBUG"))
+          std::fprintf(stderr,
+                       "faml plan: tail split of %zu of %zu row blocks at %.2f, predicted %.0f "
+                       "tile-times (whole %.0f)\n",
+                       best_k, nu, best_f, best_span, simulate(0, 0.5));
+        std::map<int, int> pbase;  // progress counters of the aggregates with split blocks
+        for (size_t i = nu - best_k; i < nu; ++i) {
+          Unit& x = rows_units[i];
+          auto it = pbase.find(x.a);
+          if (it == pbase.end()) {
+            it = pbase.emplace(x.a, pb).first;
+            pb += x.T;
+          }
+          const int h = std::min(x.T - 1, std::max(1, (int)std::lround(best_f * x.T)));
+          Unit head = x;
+          head.pb = it->second;
+          head.word = unit_word(kUnitRowSeg, 0, h);
+          head.est = -3.0;
+          x.pb = it->second;
+          x.word = unit_word(kUnitRowSeg, h, x.T);
+          x.est = -1.0;
+          us.push_back(head);
+        }
+        for (size_t i = 0; i < nu - best_k; ++i) rows_units[i].est = -2.0;
+        pl->tail_split = (int)best_k;
+      }
+    }
     // row blocks have no dependencies and each spans its aggregate's whole width (or
     // the members before a band): first in the queue (measured on per-rank shares of
     // C4: N = 4 69 ms per iteration against 80 ms when spread among the sweeps)
@@ -1352,6 +1511,10 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
                          nr, pl->irows.p, init, pl->Xa.p, pl->Fprev.p);
       GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
+      if (pl->pull.p && pl->nrows > 0)  // cA is fixed for the whole call
+        hipLaunchKernelGGL((pull_precompute_kernel<D>), dim3((pl->nrows + 3) / 4), dim3(256), 0,
+                           ss, pl->nrows, pl->rows.p, pl->pt_ix, pl->ip, pl->ecode.p, pl->vA, cA,
+                           pl->pull.p);
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
@@ -1368,7 +1531,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           GE_HIP(hipEventRecord(re[0], ss));
         }
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
-                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
+                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c, pl->pull.p};
         // the heavy member rows' segment terms need only `cur`: queued beside the
         // repulsion launch (ge_rows.hpp launch_rows_early)
         const bool rows_early =

@@ -64,6 +64,7 @@ struct RowClasses {
   const long long* hoff = nullptr;
   int seg_mode = 0;               // kSegBinade / kSegStore when nseg > 0
   int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0, nseg = 0;
+  int xcd = 1;       // tile_rows_kernel deals tiles XCD-major (xcd_major; GE_ROWS_XCD=0: off)
   int tile_off = 0;  // where tile_ptr starts in the host array
   int seg_off = 0;   // where seg starts in the host array
   int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
@@ -90,6 +91,8 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
                           std::vector<int>* heavy_deg = nullptr) {
   bool tiles = ids.size() >= (size_t)kTileMinRows;
   if (const char* e = std::getenv("GE_ROWS_TILES")) tiles = std::atoi(e) != 0;
+  rc.xcd = 1;
+  if (const char* e = std::getenv("GE_ROWS_XCD")) rc.xcd = std::atoi(e) != 0;
   // few rows (a small level): latency, not throughput -- rows of more than 4
   // entries take a wave (n = 536: attraction 26 -> 13 us per iteration)
   int med = ids.size() <= 65536 ? 4 : kMedDeg, heavy = tiles ? kTileCap : kHeavyDeg;
@@ -622,10 +625,23 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p) {
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
 // Block b + first: a tile (< ntiles) or a heavy-row segment after them; `first`
 // lets the segments run as their own launch (kSegStore, beside the tiles).
+//
+// XCD-aware order (round 5): blocks are dealt round-robin over the 8 XCDs (blocks b
+// and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so with block b =
+// tile b every XCD's L2 sees every tile's gathers.  Block b takes tile
+// xcd_major(b) instead: the blocks of one XCD walk one contiguous eighth of the tile
+// list in dispatch order, so the rows whose neighbours sit close together (the
+// members of one aggregate, stored together) are gathered through one L2.
+// GE_ROWS_XCD=0 keeps b (A/B; the host passes xcd = 0).
+__device__ __forceinline__ int xcd_major(int b, int n) {
+  const int q = n >> 3, r = n & 7, x = b & 7;
+  return x * q + min(x, r) + (b >> 3);
+}
+
 template <int D, class P>
 __global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int first = 0) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
-  const int b = (int)blockIdx.x + first;
+  const int b = (L.xcd ? xcd_major((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) + first;
   if (b < L.ntiles)
     tile_rows<D>(L, p, b, lds);
   else if (L.seg_mode == kSegStore)

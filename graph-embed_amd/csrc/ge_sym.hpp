@@ -274,7 +274,18 @@ __device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int
     }
     wave_lds_sync();
     if (rows_ok && __all(ok)) {
-      for (int jj = 0; jj < cnt; ++jj)  // the j == i term is +-0 (ge_pair.hpp)
+      // two partners per iteration: their terms are independent instruction chains
+      // the scheduler can interleave; the adds stay in partner order
+      int jj = 0;
+      for (; jj + 1 < cnt; jj += 2) {  // the j == i term is +-0 (ge_pair.hpp)
+        double t0[D], t1[D];
+        rep_term<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, t0);
+        rep_term<D, true, REPEL_ONE>(xi, &tile[(jj + 1) * WV], di, tile[(jj + 1) * WV + D], repel,
+                                     t1);
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc[k] = (acc[k] + t0[k]) + t1[k];
+      }
+      if (jj < cnt)
         rep_pair<D, true, REPEL_ONE>(xi, &tile[jj * WV], di, tile[jj * WV + D], repel, acc);
     } else {
       for (int jj = 0; jj < cnt; ++jj)

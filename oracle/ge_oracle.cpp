@@ -15,6 +15,7 @@
 #include "ge_oracle.h"
 
 #include <algorithm>
+#include <cassert>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -23,6 +24,7 @@
 #include <map>
 #include <random>
 #include <tuple>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -551,6 +553,222 @@ orc_hier* orc_partition(int n, const int* I, const int* J, const double* D, doub
     }
     if (progress && (++rounds % 50) == 0)
       std::fprintf(stderr, "orc_partition: round %ld M %d levels %zu\n", rounds, M,
+                   h->rows.size());
+  } while (1.0 * M / M_prev < stall);
+  snapshot();
+  return h;
+}
+
+// The same loop (src/partitioner.cpp:1550-1893) with the per-vertex std::map
+// replaced by an unordered entry list, for the C4 digest: the std::map version
+// spends hours chasing tree nodes in the scans (~7 s per round at C4, 9 969 rounds).
+// Every operation of the loop above is performed in the same order on the same
+// cells; only the container differs, and nothing the loop computes depends on the
+// container's iteration order:
+//   * scan (:1703-1726): the reference walks a[i] in ascending j and keeps the
+//     first strict maximum, i.e. the smallest j among the entries with the largest
+//     eta; an unordered walk keeps (eta > top) or (eta == top and j < arg), which is
+//     the same entry (eta is finite: weights / T and alpha products), and top is that
+//     entry's eta either way;
+//   * contraction (:1756-1779): one merge touches, for each neighbour k of j', the
+//     cells a[k][j'] (erased), a[i'][k] and a[k][i'] (one += each) and best_eta[k];
+//     distinct k touch distinct cells, so the walk order of a[j'] changes no value
+//     (across merges the order is the merge order, as above);
+//   * representative choice (:1737-1743): list sizes only.
+// a[i][k] += w on a missing key inserts 0.0 and adds, as std::map::operator[] does.
+// tests/test_oracle.py checks it against orc_partition on R-MAT / ER graphs with
+// every option, and tests/golden/make_partition_digest.py reproduces the committed
+// C3 digest (std::map version) before it runs C4.
+namespace {
+struct FlatAdj {
+  std::vector<int> key;
+  std::vector<double> w;
+  std::unordered_map<int, int>* idx = nullptr;  // key -> slot, for long lists
+  static constexpr size_t kIndexAt = 48;
+  ~FlatAdj() { delete idx; }
+  int find(int k) const {
+    if (idx) {
+      auto it = idx->find(k);
+      return it == idx->end() ? -1 : it->second;
+    }
+    for (size_t s = 0; s < key.size(); ++s)
+      if (key[s] == k) return (int)s;
+    return -1;
+  }
+  void erase(int k) {  // the key is present (:1763 dereferences find)
+    const int s = find(k);
+    assert(s >= 0);
+    const int last = (int)key.size() - 1;
+    if (s != last) {
+      key[s] = key[last];
+      w[s] = w[last];
+      if (idx) (*idx)[key[s]] = s;
+    }
+    key.pop_back();
+    w.pop_back();
+    if (idx) idx->erase(k);
+  }
+  void insert(int k, double v) {  // a new key with its value (std::map::insert)
+    key.push_back(k);
+    w.push_back(0.0);
+    w.back() = v;
+    if (idx) {
+      (*idx)[k] = (int)key.size() - 1;
+    } else if (key.size() > kIndexAt) {
+      idx = new std::unordered_map<int, int>();
+      idx->reserve(2 * key.size());
+      for (size_t q = 0; q < key.size(); ++q) (*idx)[key[q]] = (int)q;
+    }
+  }
+  void add(int k, double v) {  // a[i][k] += v
+    int s = find(k);
+    if (s < 0) {
+      s = (int)key.size();
+      key.push_back(k);
+      w.push_back(0.0);
+      if (idx) {
+        (*idx)[k] = s;
+      } else if (key.size() > kIndexAt) {
+        idx = new std::unordered_map<int, int>();
+        idx->reserve(2 * key.size());
+        for (size_t q = 0; q < key.size(); ++q) (*idx)[key[q]] = (int)q;
+      }
+    }
+    w[s] = w[s] + v;
+  }
+};
+}  // namespace
+
+orc_hier* orc_partition_flat(int n, const int* I, const int* J, const double* D, double cf,
+                             int positive_merging, double stall, int matching_iterations) {
+  const double inf = std::numeric_limits<double>::infinity();
+  auto* h = new orc_hier();
+  int N = n, M = n;
+
+  std::vector<FlatAdj> adj(n);  // :1561-1577 (duplicate entries of a row: the map keeps the first)
+  std::vector<double> alpha(n);
+  for (int i = 0; i < n; ++i) {
+    double s = 0.0;
+    for (int e = I[i]; e < I[i + 1]; ++e) {
+      if (J[e] != i && adj[i].find(J[e]) < 0) adj[i].insert(J[e], D[e]);
+      s += D[e];
+    }
+    alpha[i] = s;
+  }
+  double T = 0.0;  // :1580-1591
+  for (int i = 0; i < n; ++i)
+    for (int e = I[i]; e < I[i + 1]; ++e) T += D[e];
+  for (int i = 0; i < n; ++i) alpha[i] /= T;
+
+  std::vector<int> basis(n), used(n), pos(n), parent(n);
+  for (int i = 0; i < n; ++i) basis[i] = used[i] = pos[i] = parent[i] = i;
+  auto root_of = [&](int x) {  // :1622-1633
+    int r = x;
+    while (parent[r] != r) r = parent[r];
+    while (parent[x] != r) {
+      int nx = parent[x];
+      parent[x] = r;
+      x = nx;
+    }
+    return r;
+  };
+  std::vector<double> best_eta(n, -inf), best_ind(n, 0.0);
+  std::vector<char> touched(n, 0);
+
+  auto snapshot = [&]() {  // :1797-1815 / :1840-1852 + interpolationMatrix :29-65
+    std::vector<std::vector<int>> groups(M);
+    for (int y = 0; y < (int)basis.size(); ++y) groups[pos[root_of(basis[y])]].push_back(y);
+    std::vector<int> ip(M + 1), ix;
+    ix.reserve(N);
+    ip[0] = 0;
+    for (int r = 0; r < M; ++r) {
+      for (int y : groups[r]) ix.push_back(y);
+      ip[r + 1] = (int)ix.size();
+    }
+    h->rows.push_back(M);
+    h->cols.push_back(N);
+    h->indptr.push_back(std::move(ip));
+    h->indices.push_back(std::move(ix));
+  };
+
+  const bool progress = std::getenv("ORC_PROGRESS") != nullptr;
+  long rounds = 0;
+  int M_prev = M;
+  do {
+    std::vector<std::pair<int, int>> merges;
+    for (int pass = 0; pass < matching_iterations; ++pass) {
+#pragma omp parallel for schedule(dynamic, 512)
+      for (int x = 0; x < (int)used.size(); ++x) {  // :1703-1726
+        const int i = used[x];
+        if (touched[i] && best_eta[i] != -inf) continue;
+        double top = -inf;
+        int arg = -1;
+        const FlatAdj& a = adj[i];
+        const double ai = alpha[i];
+        for (size_t s = 0; s < a.key.size(); ++s) {
+          const int k = a.key[s];
+          if (touched[k]) continue;
+          double eta = 2 * (a.w[s] / T - ai * alpha[k]);
+          if (eta > top || (eta == top && k < arg)) {
+            top = eta;
+            arg = k;
+          }
+        }
+        best_eta[i] = top;
+        best_ind[i] = arg;
+      }
+      for (int x = 0; x < (int)used.size(); ++x) {  // :1728-1753
+        const int i = used[x];
+        if (touched[i]) continue;
+        const int j = (int)best_ind[i];
+        if (j == -1 || touched[j] || best_eta[i] < best_eta[j]) continue;
+        if (positive_merging && !(best_eta[i] > 0)) continue;
+        if (adj[i].key.size() < adj[j].key.size())
+          merges.push_back(std::make_pair(j, i));
+        else
+          merges.push_back(std::make_pair(i, j));
+        touched[i] = touched[j] = 1;
+      }
+    }
+    for (const auto& mg : merges) {  // :1756-1779
+      const int keep = mg.first, gone = mg.second;
+      const FlatAdj& g = adj[gone];
+      for (size_t s = 0; s < g.key.size(); ++s) {
+        const int k = g.key[s];
+        const double wk = g.w[s];
+        adj[k].erase(gone);
+        best_eta[k] = -inf;
+        if (k == keep) {
+          alpha[keep] = alpha[keep] + alpha[gone];
+        } else {
+          adj[keep].add(k, wk);
+          adj[k].add(keep, wk);
+        }
+      }
+    }
+    M_prev = M;
+    if (1.0 * M / N <= cf) {
+      snapshot();
+      basis = used;
+      N = M;
+    }
+    for (const auto& mg : merges) {  // :1819-1834
+      const int keep = mg.first, gone = mg.second;
+      const int slot = pos[gone];
+      const int last = used.back();
+      std::swap(used[slot], used[used.size() - 1]);
+      used.pop_back();
+      pos[last] = slot;
+      parent[gone] = keep;
+      touched[keep] = 0;
+      M -= 1;
+      std::vector<int>().swap(adj[gone].key);  // j' is never read again
+      std::vector<double>().swap(adj[gone].w);
+      delete adj[gone].idx;
+      adj[gone].idx = nullptr;
+    }
+    if (progress && (++rounds % 50) == 0)
+      std::fprintf(stderr, "orc_partition_flat: round %ld M %d levels %zu\n", rounds, M,
                    h->rows.size());
   } while (1.0 * M / M_prev < stall);
   snapshot();

@@ -83,6 +83,10 @@ typedef struct orc_hier orc_hier;
 orc_hier* orc_partition(int n, const int* indptr, const int* indices, const double* data,
                         double coarsening_factor, int positive_merging,
                         double stall_stop_threshold, int matching_iterations);
+/* the same loop over unordered entry lists (ge_oracle.cpp: identical results, faster) */
+orc_hier* orc_partition_flat(int n, const int* indptr, const int* indices, const double* data,
+                        double coarsening_factor, int positive_merging,
+                        double stall_stop_threshold, int matching_iterations);
 int orc_hier_levels(const orc_hier* h);
 /* rows/cols of P_T[l]; indptr has rows+1 entries, indices has cols entries */
 void orc_hier_shape(const orc_hier* h, int l, int* rows, int* cols);

@@ -28,6 +28,48 @@ import ge_amd as ge  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 
 
+def bfs_order(ip, ix, n):
+    """Cuthill-McKee order of a symmetric CSR on the device: new -> old ids."""
+    dev = ip.device
+    deg = torch.diff(ip).to(torch.int64)
+    rank = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    src = int(torch.argmax(deg).item())
+    rank[src] = 0
+    frontier = torch.tensor([src], dtype=torch.int64, device=dev)
+    nxt = 1
+    big = torch.iinfo(torch.int64).max
+    while frontier.numel():
+        cnt = deg[frontier]
+        tot = int(cnt.sum().item())
+        if tot == 0:
+            break
+        starts = ip[frontier].to(torch.int64)
+        off = torch.cumsum(cnt, 0) - cnt
+        ent = torch.repeat_interleave(starts - off, cnt) + torch.arange(tot, device=dev)
+        nb = ix[ent].to(torch.int64)
+        del ent
+        par = torch.repeat_interleave(rank[frontier], cnt)
+        keep = rank[nb] < 0
+        nb, par = nb[keep], par[keep]
+        if nb.numel() == 0:
+            break
+        best = torch.full((n,), big, dtype=torch.int64, device=dev)
+        best.scatter_reduce_(0, nb, par, reduce="amin")
+        newv = torch.unique(nb)
+        del nb, par
+        key = best[newv] * n + newv
+        newv = newv[torch.argsort(key)]
+        del best, key
+        rank[newv] = nxt + torch.arange(newv.numel(), device=dev)
+        nxt += newv.numel()
+        frontier = newv
+    rest = torch.nonzero(rank < 0).flatten()
+    rank[rest] = nxt + torch.arange(rest.numel(), device=dev)
+    order = torch.empty(n, dtype=torch.int64, device=dev)
+    order[rank] = torch.arange(n, device=dev)
+    return order
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100_000_000)
@@ -35,11 +77,14 @@ def main():
     ap.add_argument("--seed", type=int, default=12345)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--relabel", choices=["none", "degree"], default="none",
-                    help="degree: vertices renumbered by descending degree (stable), rows "
-                         "and coordinates permuted alike, each row's entry order kept; the "
-                         "pass's results are the same values at permuted positions "
-                         "(checked against the unpermuted pass)")
+    ap.add_argument("--relabel", choices=["none", "degree", "bfs"], default="none",
+                    help="degree: vertices renumbered by descending degree (stable); bfs: "
+                         "Cuthill-McKee order (breadth-first from the largest hub, each "
+                         "level's vertices by their first parent's rank, then id; vertices "
+                         "it does not reach after them in id order).  Rows and coordinates "
+                         "permuted alike, each row's entry order kept; the pass's results "
+                         "are the same values at permuted positions (checked against the "
+                         "unpermuted pass)")
     a = ap.parse_args()
     dim = 3
     t0 = time.perf_counter()
@@ -61,13 +106,16 @@ def main():
         ((deg + 1) * 1e6)[:, None]
     y = torch.empty_like(x)
     check = None
-    if a.relabel == "degree":
+    if a.relabel != "none":
         t0 = time.perf_counter()
         plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), dim, 0, n)
         plan.attract(x.data_ptr(), frep.data_ptr(), y.data_ptr())
         ctx.sync()
         plan.close()
-        order = torch.sort(torch.diff(ip), descending=True, stable=True).indices  # new -> old
+        if a.relabel == "degree":
+            order = torch.sort(torch.diff(ip), descending=True, stable=True).indices  # new -> old
+        else:
+            order = bfs_order(ip, ix, n)
         new_id = torch.empty_like(order)
         new_id[order] = torch.arange(n, device=dev)
         dn = torch.diff(ip)[order]
@@ -81,7 +129,7 @@ def main():
         ip = ip2.to(torch.int32)
         x, frep = x[order].contiguous(), frep[order].contiguous()
         check = y[order].clone()
-        print(f"relabelled by degree in {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+        print(f"relabelled ({a.relabel}) in {time.perf_counter() - t0:.1f}s", file=sys.stderr,
               flush=True)
     t0 = time.perf_counter()
     plan = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), dim, 0, n)

@@ -5,7 +5,7 @@ hierarchy of a configs[] graph as level sizes + sha256 of the P_T arrays.
       (~21 minutes serial here, 2025; the scan is OpenMP-parallel like the
       reference's :1703 since round 3)
   c4  configs[3]: LCC of the R-MAT with 10M ids, 80M draws, seed 12345
-      (hours on 8 cores; run it in the background)
+      (--flat: 22 minutes on 5 threads here; the std::map oracle ~18 h)
 
 The oracle (oracle/ge_oracle.cpp, the reference loop of src/partitioner.cpp:1550-1893
 restated with its std::map adjacency) is far too slow to run inside a test at
@@ -14,7 +14,7 @@ tests/test_partition_device.py::test_partition_device_<cfg>_digest checks the
 device hierarchy against it.  The per-level sha256 values let a mismatch be
 localised to the first differing level.
 
-usage: python tests/golden/make_partition_digest.py [c3|c4] [--host]
+usage: python tests/golden/make_partition_digest.py [c3|c4] [--host | --flat]
 
 --host: the library's host path (csrc/ge_partition.cpp: the same rounds with
 incremental rescans, bit-exact with the oracle on every fixture) instead of the
@@ -22,6 +22,11 @@ oracle.  The oracle restates the reference's rescan of every untouched vertex in
 every pass (:1703-1726), which at C4 runs ~5 s per round for 9 969 rounds (measured
 here: 1 000 rounds in 2 h on 6 threads), so the C4 digest comes from the host path,
 pinned first by reproducing the oracle's committed C3 digest in the same run.
+
+--flat (round 5): the oracle's own loop with the per-vertex std::map replaced by
+unordered entry lists (orc_partition_flat: every operation in the same order, only
+the container differs; tests/test_oracle.py::test_partition_flat_equals_map).  It first
+reproduces the committed C3 digest of the std::map oracle, then runs the C4 graph.
 """
 import hashlib
 import json
@@ -63,6 +68,7 @@ def lcc(cfg):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     host = "--host" in sys.argv
+    flat = "--flat" in sys.argv
     cfg = args[0] if args else "c3"
     n_ids, draws = CONFIGS[cfg]
     seed, cf = 12345, 0.125
@@ -79,10 +85,20 @@ def main():
         print("host path at C3:", pinned, flush=True)
         if got != c3["sha256"]:
             raise SystemExit("host path differs from the oracle at C3")
+    if flat and cfg != "c3":
+        with open(os.path.join(HERE, "partition_c3_digest.json")) as f:
+            c3 = json.load(f)
+        t = time.time()
+        got, _ = digest(O.partition(lcc("c3"), cf, flat=True))
+        pinned = {"c3_sha256": got, "equals_oracle_c3_digest": got == c3["sha256"],
+                  "seconds": round(time.time() - t, 1)}
+        print("flat oracle at C3:", pinned, flush=True)
+        if got != c3["sha256"]:
+            raise SystemExit("flat oracle differs from the std::map oracle at C3")
     L = lcc(cfg)
     print(f"{cfg}: LCC n={len(L[0]) - 1} nnz={len(L[1])}", flush=True)
     t = time.time()
-    ho = ge.partition(L, cf) if host else O.partition(L, cf)
+    ho = ge.partition(L, cf) if host else O.partition(L, cf, flat=flat)
     el = time.time() - t
     if os.environ.get("GE_DIGEST_SAVE"):  # keep the hierarchy itself (not committed)
         np.savez(os.environ["GE_DIGEST_SAVE"],
@@ -93,10 +109,14 @@ def main():
            "level_sha256": per, "seconds": round(el, 1),
            "threads": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count())),
            "method": ("library host path (csrc/ge_partition.cpp), pinned to the oracle by "
-                      "the C3 digest" if host else "oracle (oracle/ge_oracle.cpp orc_partition)"),
-           "generator": f"tests/golden/make_partition_digest.py {cfg}" + (" --host" if host else "")}
+                      "the C3 digest" if host else
+                      "oracle (oracle/ge_oracle.cpp orc_partition_flat: the reference loop over "
+                      "unordered entry lists)" if flat else
+                      "oracle (oracle/ge_oracle.cpp orc_partition)"),
+           "generator": f"tests/golden/make_partition_digest.py {cfg}" +
+                        (" --host" if host else " --flat" if flat else "")}
     if pinned:
-        out["host_path_pin"] = pinned
+        out["flat_oracle_pin" if flat else "host_path_pin"] = pinned
     with open(os.path.join(HERE, f"partition_{cfg}_digest.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(out)

@@ -63,6 +63,8 @@ def lib():
         L.orc_partition.restype = ctypes.c_void_p
         L.orc_partition.argtypes = [ctypes.c_int, _i32p, _i32p, _f64p, ctypes.c_double,
                                     ctypes.c_int, ctypes.c_double, ctypes.c_int]
+        L.orc_partition_flat.restype = ctypes.c_void_p
+        L.orc_partition_flat.argtypes = L.orc_partition.argtypes
         L.orc_hier_levels.argtypes = [ctypes.c_void_p]
         L.orc_hier_shape.argtypes = [ctypes.c_void_p, ctypes.c_int,
                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -207,11 +209,13 @@ def force_atlas_ml(A, PT, vertex_A, coords_A, r_A, dim, iterations=100, seed=0, 
     return X
 
 
-def partition(A, cf, positive_merging=True, stall=1.0, matching=2):
-    """Returns a list of P_T as (indptr, indices, rows, cols)."""
+def partition(A, cf, positive_merging=True, stall=1.0, matching=2, flat=False):
+    """Returns a list of P_T as (indptr, indices, rows, cols).  flat: the same loop
+    over unordered entry lists (orc_partition_flat: identical results, for C4)."""
     ip, ix, dx = _csr(A)
     L = lib()
-    h = L.orc_partition(len(ip) - 1, ip, ix, dx, cf, int(positive_merging), stall, matching)
+    fn = L.orc_partition_flat if flat else L.orc_partition
+    h = fn(len(ip) - 1, ip, ix, dx, cf, int(positive_merging), stall, matching)
     out = []
     for l in range(L.orc_hier_levels(h)):
         r, c = ctypes.c_int(), ctypes.c_int()

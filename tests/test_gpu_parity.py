@@ -603,6 +603,32 @@ def test_faml_segmented_row_blocks(ctx, oracle, monkeypatch, seg, dim, repel):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("k,f,dim,repel", [("100000", "0.5", 3, 1.0), ("100000", "0.9", 3, 2.0 ** 70),
+                                           ("7", "0.1", 3, 1.5), ("100000", "0.6", 2, 1.0),
+                                           ("3", "0.7", 4, 1.0)])
+def test_faml_tail_split_row_blocks(ctx, oracle, monkeypatch, k, f, dim, repel):
+    """Tail split (ge_faml.hip faml_plan_build): the k smallest row blocks of an
+    all-row-block plan cut into a head segment (columns [0, 64 round(f T))) at the
+    front of the queue and a tail segment continuing the rows' sums at its end;
+    every block cut or a few, heads of one tile (f = 0.1 on small aggregates), the
+    `/` path, every dimension."""
+    monkeypatch.setenv("GE_FAML_SYM", "1")
+    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "1e9")  # every streamed aggregate as row blocks
+    monkeypatch.setenv("GE_FAML_TAILSPLIT_K", k)
+    monkeypatch.setenv("GE_FAML_TAILSPLIT_F", f)
+    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 10 * n, seed=19), [(3, 2000), (70, 3000)], seed=dim)
+    PT = _block_partition(n, sizes, seed=8)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m + 3)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=31, repel=repel)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=31, repel=repel)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("bands,dim,repel", [
     ("2", 3, 1.0), ("3", 3, 1.0), ("4", 3, 1.5), ("8", 3, 1.0), ("2", 3, 2.0 ** 70),
     ("3", 2, 1.0), ("4", 4, 0.75), ("2", 1, 1.0)])

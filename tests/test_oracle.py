@@ -98,6 +98,39 @@ def test_partition(oracle, cf):
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
 
 
+@pytest.mark.parametrize("case", ["rmat", "hubs", "er", "weights", "nopos", "stall", "match3"])
+def test_partition_flat_equals_map(oracle, case):
+    """orc_partition_flat (unordered entry lists, used for the C4 digest) against
+    orc_partition (the reference's std::map): identical hierarchies with every
+    option, fractional weights (several entries of equal eta), hub lists past the
+    index threshold."""
+    kw = {}
+    if case == "er":
+        A = G.erdos_renyi(1500, 0.008, seed=3)
+    elif case == "hubs":
+        A = G.with_hubs(G.largest_component(G.rmat(3000, 20000, seed=8)), [(5, 1500), (9, 800)])
+    else:
+        A = G.largest_component(G.rmat(4000, 30000, seed=10))
+    if case == "weights":  # symmetric weights from a few values: ties in eta
+        ip, ix, dx = A
+        rows = np.repeat(np.arange(len(ip) - 1), np.diff(ip))
+        w = 1.0 + ((np.minimum(rows, ix) * 7 + np.maximum(rows, ix) * 13) % 3) * 0.5
+        A = (ip, ix, w)
+    if case == "nopos":
+        kw = dict(positive_merging=False)
+    if case == "stall":
+        kw = dict(stall=0.97)
+    if case == "match3":
+        kw = dict(matching=3)
+    for cf in (0.125, 0.4):
+        hm = oracle.partition(A, cf, **kw)
+        hf = oracle.partition(A, cf, flat=True, **kw)
+        assert len(hm) == len(hf) >= 1
+        for a, b in zip(hm, hf):
+            assert a[2:] == b[2:]
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
 def test_partition_shapes_chain(oracle):
     A = G.largest_component(G.rmat(2000, 14000, seed=7))
     hier = oracle.partition(A, 0.125)

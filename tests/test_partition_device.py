@@ -142,7 +142,9 @@ def test_partition_device_c3_digest(ctx):
 
 def test_partition_device_c4_digest(ctx):
     """configs[3] (the headline): LCC of the R-MAT(10M ids, 80M draws, seed 12345),
-    4.39M vertices, 9 969 rounds -- the hierarchy digest of the library's host path
-    (csrc/ge_partition.cpp), which reproduced the oracle's C3 digest in the same run
-    (the oracle's full rescans need ~18 h here at C4; make_partition_digest.py)."""
+    4.39M vertices, 9 969 rounds -- the oracle's hierarchy digest (orc_partition_flat:
+    the reference loop over unordered entry lists, 1 327 s on 5 threads here; it
+    reproduced the std::map oracle's C3 digest in the same run; make_partition_digest.py
+    --flat).  The library's host path (csrc/ge_partition.cpp) gave the same digest in
+    round 4."""
     _check_digest(ctx, "partition_c4_digest.json")
