@@ -370,10 +370,6 @@ struct FaRows {
   const double *dx, *X, *dp1, *Frep;
   double *Fprev, *Xnext;
   FaConst c;
-  // optional gather copy (plan_gather_copy): the coordinates in degree order and
-  // the CSR indices remapped to it, for the neighbour gathers only
-  const int* gix = nullptr;
-  const double* Xg = nullptr;
   struct State {
     int i, e0, e1;
     double xi[D], acc[D], fprev[D], dip1;
@@ -396,8 +392,8 @@ struct FaRows {
     // the neighbour's coordinates into registers first: all of a tile thread's
     // gathers issue before any domain test (C5: 37.9 -> 31.2 ms per pass)
     double xv[D];
-    const double* src = Xg ? Xg : X;  // same values: the gather copy is a permutation
-    const size_t j = (size_t)(Xg ? gix[e] : ix[e]) * D;
+    const double* src = X;
+    const size_t j = (size_t)ix[e] * D;
 #pragma unroll
     for (int k = 0; k < D; ++k) xv[k] = src[j + k];
     const double* xj = xv;
@@ -1521,33 +1517,10 @@ void launch_grouped_step(hipStream_t s, int n, int rb, int re, const int* ip, co
 template <int D>
 void launch_attract(hipStream_t s, const RowClasses& rc, RowStreams& rs, int rb, const int* ip,
                     const int* ix, const double* dx, const double* X, const double* dp1,
-                    const double* Frep, double* Fprev, double* Xnext, const FaConst& c,
-                    const int* gix = nullptr, const double* Xg = nullptr) {
-  const FaRows<D> fr{rb, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c, gix, Xg};
+                    const double* Frep, double* Fprev, double* Xnext, const FaConst& c) {
+  const FaRows<D> fr{rb, ip, ix, dx, X, dp1, Frep, Fprev, Xnext, c};
   launch_rows<D>(rc, fr, s, rs);
 }
-
-// Gather copy of the coordinates: Xg[p] = X[inv[p]], vertices in descending
-// degree.  The neighbour gathers of the attraction pass (one random 24-B record
-// per CSR entry, a 64-B line each) then hit the copy, where the high-degree
-// vertices that receive most of the gathers share lines and stay in L2.  The
-// values are the same, so are the bits.
-template <int D>
-__global__ void gather_copy_kernel(int n, const int* __restrict__ inv, const double* __restrict__ X,
-                                   double* __restrict__ Xg) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const size_t v = (size_t)inv[p] * D;
-#pragma unroll
-  for (int k = 0; k < D; ++k) Xg[(size_t)p * D + k] = X[v + k];
-}
-
-__global__ void remap_indices_kernel(long long count, const int* __restrict__ pos,
-                                     const int* __restrict__ ix, int* __restrict__ gix) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < count) gix[e] = pos[ix[e]];
-}
-
 
 }  // namespace
 }  // namespace ge
@@ -1565,9 +1538,6 @@ struct ge_fa_plan {
   ge::FaConst c{};
   ge::DevBuf<double> dp1, frep, fprev, fpart;
   ge::DevBuf<int> rows;  // rb..re in degree classes (ge_rows.hpp)
-  ge::DevBuf<int> ginv, gix;  // gather copy: vertex of each position, remapped CSR indices
-  ge::DevBuf<double> xg;
-  long long gbase = 0;        // ip[rb]: gix covers the entries of rows [rb, re)
   ge::RowClasses rc;
   ge::RowStreams rstreams;
   int cus = 256;
@@ -1633,36 +1603,9 @@ static void plan_init(ge_fa_plan* pl) {
     pl->sym = !off && pl->p.mode == GE_MODE_STRICT && pl->rb == 0 && pl->re == pl->n &&
               (force || pl->n > stream_max());
   }
-  // Gather copy, opt-in (GE_GATHER_COPY=1).  Measured without benefit: C2 attraction
-  // 0.324 ms with it against 0.301 ms without, C5 31.8 against 30.3 ms; L2 misses
-  // fell 14 % (FETCH 697 MB per C2 pass) but the long tail of low-degree
-  // neighbours still costs one random line each.
-  bool gather = false;
-  if (const char* e = std::getenv("GE_GATHER_COPY")) gather = *e && *e != '0';
-  if (gather && rows > 0) {
-    std::vector<int> h_ip(pl->n + 1);
-    GE_HIP(hipMemcpyAsync(h_ip.data(), pl->ip, sizeof(int) * (pl->n + 1), hipMemcpyDeviceToHost, s));
-    GE_HIP(hipStreamSynchronize(s));
-    std::vector<int> inv(pl->n), pos(pl->n);
-    std::iota(inv.begin(), inv.end(), 0);
-    std::stable_sort(inv.begin(), inv.end(), [&](int a, int b) {
-      return h_ip[a + 1] - h_ip[a] > h_ip[b + 1] - h_ip[b];
-    });
-    for (int q = 0; q < pl->n; ++q) pos[inv[q]] = q;
-    pl->gbase = h_ip[pl->rb];
-    const long long cnt = (long long)h_ip[pl->re] - h_ip[pl->rb];
-    pl->ginv.alloc(pl->n);
-    pl->ginv.upload(inv.data(), pl->n, s);
-    pl->xg.alloc((size_t)pl->n * pl->dim);
-    pl->gix.alloc(std::max(cnt, 1ll));
-    DevBuf<int> dpos(pl->n);
-    dpos.upload(pos.data(), pl->n, s);
-    if (cnt > 0)
-      hipLaunchKernelGGL(remap_indices_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
-                         cnt, dpos.p, pl->ix + pl->gbase, pl->gix.p);
-    GE_HIP(hipGetLastError());
-    GE_HIP(hipStreamSynchronize(s));
-  }
+  // (Round 4 also built a degree-ordered gather copy of the coordinates for the
+  // neighbour gathers: C2 0.324 against 0.301 ms per pass, C5 31.8 against 30.3 ms;
+  // removed in round 5)
 }
 
 // The symmetric path's units, progress counters and hand-over buffer (n x d), made
@@ -1696,13 +1639,6 @@ static void sym_prepare(ge_fa_plan* pl) {
   }
 }
 
-// Refresh the gather copy from this iteration's coordinates (before the row kernels).
-template <int D>
-static void plan_gather_copy(ge_fa_plan* pl, const double* xc, hipStream_t s) {
-  if (!pl->xg.p) return;
-  hipLaunchKernelGGL(gather_copy_kernel<D>, dim3((pl->n + 255) / 256), dim3(256), 0, s, pl->n,
-                     pl->ginv.p, xc, pl->xg.p);
-}
 
 // A symmetric launch whose hand-over wait timed out (seen through the pinned
 // error word, without a synchronisation) fails the next step or the run's end.
@@ -1750,10 +1686,8 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
                           pl->frep.p, pl->fpart.p, pl->cus);
     }
     if (ev) GE_HIP(hipEventRecord(ev[1], s));
-    plan_gather_copy<D>(pl, xc, s);
     launch_attract<D>(s, pl->rc, pl->rstreams, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, pl->frep.p,
-                      pl->fprev.p, xn, pl->c, pl->gix.p ? pl->gix.p - pl->gbase : nullptr,
-                      pl->xg.p);
+                      pl->fprev.p, xn, pl->c);
   });
   GE_HIP(hipGetLastError());
   if (ev) GE_HIP(hipEventRecord(ev[2], s));
@@ -1779,10 +1713,8 @@ static void plan_attract(ge_fa_plan* pl, const double* xc, const double* frep, d
   }
   dispatch_dim(pl->dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    plan_gather_copy<D>(pl, xc, s);
     launch_attract<D>(s, pl->rc, pl->rstreams, pl->rb, pl->ip, pl->ix, pl->dx, xc, pl->dp1.p, frep,
-                      pl->fprev.p, xn, pl->c, pl->gix.p ? pl->gix.p - pl->gbase : nullptr,
-                      pl->xg.p);
+                      pl->fprev.p, xn, pl->c);
   });
   GE_HIP(hipGetLastError());
   if (ev) GE_HIP(hipEventRecord(ev[2], s));

@@ -507,51 +507,12 @@ __global__ void edge_code_kernel(int nrows, const int* __restrict__ rows,
   }
 }
 
-// The static part of every external pull of the streamed members (one wave per
-// row): pull[e] = ((cA[b] - cA[a]) / dis_ab) * 100 for k < D (include/forceatlas.hpp
-// :453-465: direction * Fao_ij, evaluated left to right before the division by
-// mag), and pull[e][D] = 1.0 when cA[a] and cA[b] are in the shared-reciprocal
-// domain (the condition under which pull_edge used div_by).  Computed with `/`,
-// which equals div_by in that domain, so FamlRows::term gets pull_edge's bits.
-template <int D>
-__global__ void __launch_bounds__(256)
-pull_precompute_kernel(int nrows, const int* __restrict__ rows, const int* __restrict__ pt_ix,
-                       const int* __restrict__ ip, const int* __restrict__ ecode,
-                       const int* __restrict__ vA, const double* __restrict__ cA,
-                       double* __restrict__ pull) {
-  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (q >= nrows) return;
-  const int v = pt_ix[rows[q]];
-  const double* ca = cA + (size_t)vA[v] * D;
-  const bool ca_ok = all_coord_ok<D>(ca);
-  for (int e = ip[v] + lane; e < ip[v + 1]; e += 64) {
-    const int code = ecode[e];
-    if (code >= 0) continue;
-    const double* cb = cA + (size_t)(-code - 1) * D;
-    double t[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) t[k] = cb[k] - ca[k];
-    double qd = t[0] * t[0];
-#pragma unroll
-    for (int k = 1; k < D; ++k) qd = qd + t[k] * t[k];
-    const double dis = clamp_eps(sqrt(qd));
-    double* pu = pull + (size_t)e * (D + 1);
-#pragma unroll
-    for (int k = 0; k < D; ++k) pu[k] = (t[k] / dis) * 100.0;
-    pu[D] = (ca_ok && all_coord_ok<D>(cb)) ? 1.0 : 0.0;
-  }
-}
-
 template <int D>
 struct FamlRows {
   const int *pt_ip, *pt_ix, *ecode, *ip, *vA;
   const double *dx, *cA, *Xc, *DP, *Fscr;
   double *Xn, *Fprev;
   MlConst c;
-  // per CSR entry e of a streamed member, D + 1 doubles (pull_precompute_kernel):
-  // the external pull's ((cA[b] - cA[a]) / dis) * 100, static while cA is, and 1.0
-  // when cA[a] and cA[b] are in the shared-reciprocal domain; nullptr: gathered
-  const double* pull = nullptr;
   struct State {
     int cpos, a, li, e0, e1;
     double xi[D], acc[D], fprev[D], dip1, mag;
@@ -583,23 +544,6 @@ struct FamlRows {
   }
   __device__ __forceinline__ void term(const State& s, int e, double (&t)[D]) const {
     const int code = ecode[e];
-    if (pull && code < 0) {
-      // external pull (:453-465) with its static part precomputed: the term is
-      // (direction * 100) / mag, and only the division by the row's mag is left --
-      // the same division, on the same operands, as pull_edge's
-      const double* pu = pull + (size_t)e * (D + 1);
-      double u[D];
-#pragma unroll
-      for (int k = 0; k < D; ++k) u[k] = pu[k];
-      if (s.row_ok && pu[D] != 0.0) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = div_by(u[k], s.mag, s.rmag);
-      } else {
-#pragma unroll
-        for (int k = 0; k < D; ++k) t[k] = u[k] / s.mag;
-      }
-      return;
-    }
     // the neighbour's (or its aggregate's) coordinates into registers before
     // the branch, so a thread's gathers issue together
     const double* src = code >= 0 ? Xc + (size_t)code * D : cA + (size_t)(-code - 1) * D;
@@ -777,23 +721,19 @@ struct ge_faml_plan {
   int ns = 0, nm = 0, nl = 0, nhuge = 0;
   size_t off_m = 0, off_l = 0;
   ge::DevBuf<int> pos, order, beg, rows, erows, queue, huge, ecode;
-  ge::DevBuf<double> pull;  // FamlRows::pull (allocated when it fits, GE_FAML_PULL=0: off)
   ge::RowClasses ecls;
   ge::RowStreams rstreams;
   ge::DevBuf<int2> items;
   int nrows = 0, nitems = 0, R = 1, code = 0, rep_blocks = 0;
   // symmetric repulsion (ge_sym.hpp): sweep units and per-tile progress counters
   bool sym = false;
-  bool sym_pair = false;  // faml_sym_pair (one wave per block, two row tiles per unit)
   ge::DevBuf<int4> units;
   ge::DevBuf<int> prog;
   ge::DevBuf<double> hand;  // column sums handed between sweeps, component-major [dim][n]
   ge::DevBuf<int> sym_err;  // set by a hand-over wait that timed out
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
-  int banded = 0, rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
-  int tail_split = 0;  // row blocks cut into a head and a tail segment (faml_plan_build)
-  bool sym_ext = false;  // units of the band / segmented-row kinds: the EXT kernel
+  int rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
   std::string stamp_path;
@@ -930,11 +870,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::vector<int> hdeg;
     classify_rows(rows, deg, erows, pl->ecls, kSegStore, &hdeg);
     pl->ecode.alloc(std::max(h_ip[pl->n], 1));
-    {  // precomputed external pulls: (D + 1) doubles per CSR entry of the level
-      const double bytes = (double)h_ip[pl->n] * (pl->dim + 1) * sizeof(double);
-      const char* e = std::getenv("GE_FAML_PULL");
-      if (!(e && *e == '0') && bytes <= 8e9) pl->pull.alloc((size_t)h_ip[pl->n] * (pl->dim + 1));
-    }
     pl->erows.alloc(erows.size());
     pl->erows.upload(erows.data(), erows.size(), st);
     pl->ecls.bind(pl->erows.p);
@@ -979,48 +914,33 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     std::vector<int> T(big.size());
     const bool any_big = !big.empty();
     for (size_t b = 0; b < big.size(); ++b) T[b] = (h_pt_ip[big[b] + 1] - h_pt_ip[big[b]] + 63) / 64;
-    {
-      // two row tiles per wave (faml_sym_pair): bit-exact, but slower at C4 (139.8
-      // against 152.9 ms per launch: more units in flight spin longer), so opt-in
-      const char* e = std::getenv("GE_FAML_SYM_PAIR");
-      pl->sym_pair = e && *e == '1';
-    }
-    const int sym_threads = pl->sym_pair ? 64 : kSymT;
     int occ = 1;
     dispatch_dim(dim, [&](auto Dc) {
       constexpr int D = decltype(Dc)::value;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-          &occ, pl->sym_pair ? (const void*)faml_sym_pair<D, false>
-                             : (const void*)faml_sym_repulse<D, false>,
-          sym_threads, 0));
+          &occ, (const void*)faml_sym_repulse<D, false>, kSymT, 0));
     });
     // three blocks (waves) per SIMD of the four that fit: fewer units in flight spin
     // less on hand-overs (C4 N = 1: 137.2 against 138.3 ms per launch; N = 8 shares
     // 30.0 against 32.7 ms; scripts/sym_timeline.py, profiles/r03/sym_timeline)
-    int bpc = std::min(std::max(occ, 1), pl->sym_pair ? 16 : 3);
+    int bpc = std::min(std::max(occ, 1), 3);
     if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
       bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
     pl->sym_blocks = cus * bpc;
-    // a pair unit carries two row tiles: count its wave twice in the model
-    const double waves = (double)pl->sym_blocks * (sym_threads / 64) * (pl->sym_pair ? 2 : 1);
-    // Per streamed aggregate: plain sweeps (K = 1), K bands (ge_sym.hpp: pre row
-    // blocks, in-band sweeps, post row blocks), or whole row blocks (kRowsMode).
-    // The launch lasts about max(work / waves, the start of the sweeps + the longest
-    // chain) tile-times, where
-    //   sweeps:  work T^2 / 2 + T,               chain chain_k T
-    //   K bands: work sum_b (Tb^2 / 2 + Tb) + row_k sum_b Tb (T - Tb),
-    //            chain max_b (row_k b0 + chain_k Tb + row_k (T - b1)), the post
-    //            part run by each sweep's own wave after its band
-    //   rows:    work row_k T^2,                 chain row_k T
-    // (a row block evaluates every ordered pair at ~0.6 the wave time of a sweep tile;
-    // a sweep chain is ~2.5 T because each sweep starts ~2 tiles behind the one before).
+    const double waves = (double)pl->sym_blocks * (kSymT / 64);
+    // Per streamed aggregate: symmetric sweeps or whole row blocks.  The launch lasts
+    // about max(work / waves, the longest row block, the sweeps' start + the longest
+    // sweep chain) tile-times, where
+    //   sweeps:  work T^2 / 2 + T,  chain chain_k T (each sweep starts ~2 tiles behind
+    //            the one before)
+    //   rows:    work row_k T^2,    chain row_k T   (every ordered pair, no chain)
     // Whole row blocks are first in the queue, so when they hold more than the waves
-    // the sweeps start late (start = their work / waves); the pre blocks of a band
-    // are interleaved with the sweeps, each just ahead of when its column tile is due.  Greedy: while the
-    // longest chain sets the time, step its aggregate to the next option (more bands,
-    // then rows) if that lowers the prediction.  At N = 1 (C4) the launch is
-    // work-bound and nothing changes; the shares of a multi-GPU run are chain-bound.
-    constexpr int kRowsMode = 1 << 20;
+    // the sweeps start late (start = their work / waves).  The k largest aggregates
+    // run as row blocks, k minimising the prediction; no mix whose row blocks hold
+    // more than half the waves (their raised waves delay and slow the sweeps: per-rank
+    // shares of C4, N = 4: 20 of 24 aggregates as row blocks 70 ms per iteration, 7 of
+    // 25 58 ms).  At N = 1 (C4) the launch is work-bound and every aggregate sweeps;
+    // the shares of a multi-GPU run are chain-bound.
     // row_k: a row-block tile (64 x 64 ordered pairs) against a sweep tile (64 x 64
     // unordered), wave time at full load -- 0.6 measured on an N = 8 share of C4
     // (all row blocks: 17.9 us per row tile per wave, against 29.8 us per sweep tile
@@ -1028,65 +948,9 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     double chain_k = 2.5, row_k = 0.6;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
     if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
-    int force_bands = 0;  // GE_FAML_SYM_BANDS=K: every streamed aggregate in K bands (tests)
-    if (const char* e = std::getenv("GE_FAML_SYM_BANDS")) force_bands = std::max(0, std::atoi(e));
-    auto band_lo = [](int Tb, int K, int i) { return (int)((long long)Tb * i / K); };
-    auto cost_of = [&](int Tb, int K, double& work, double& chain, double& rwork) {
-      const double t = Tb;
-      if (K == kRowsMode) {
-        work = rwork = row_k * t * t;
-        chain = row_k * t;
-        return;
-      }
-      work = rwork = chain = 0.0;
-      for (int i = 0; i < K; ++i) {
-        const double b0 = band_lo(Tb, K, i), b1 = band_lo(Tb, K, i + 1), tb = b1 - b0;
-        work += 0.5 * tb * tb + tb + row_k * tb * (t - tb);
-        chain = std::max(chain, row_k * b0 + chain_k * tb + row_k * (t - b1));
-      }
-    };
-    static const int kOptions[] = {1, 2, 3, 4, 6, 8, kRowsMode};
-    std::vector<int> opt(big.size(), 0);  // index into kOptions
-    auto mode_of = [&](size_t b) {
-      if (force_bands > 0) return std::min(force_bands, std::max(1, T[b] / 2));
-      return kOptions[opt[b]];
-    };
-    auto predict = [&](size_t* crit) {
-      double work = 0.0, rwork = 0.0, runits = 0.0, chain = 0.0;
-      size_t arg = 0;
-      std::vector<double> ch(big.size());
-      for (size_t b = 0; b < big.size(); ++b) {
-        double w, c, r;
-        const int K = mode_of(b);
-        cost_of(T[b], K, w, c, r);
-        work += w;
-        rwork += r;
-        if (K == kRowsMode) runits += T[b];  // whole row blocks: first in the queue
-        ch[b] = c;
-      }
-      const double start = runits > waves ? rwork / waves : 0.0;
-      for (size_t b = 0; b < big.size(); ++b) {
-        const double c = ch[b] + (mode_of(b) == kRowsMode ? 0.0 : start);
-        if (c > chain) {
-          chain = c;
-          arg = b;
-        }
-      }
-      if (crit) *crit = arg;
-      return std::max(work / waves, chain);
-    };
-    double best = any_big ? predict(nullptr) : 0.0;
-    // Default: the round-3 rule -- the k largest aggregates as whole row blocks, k
-    // minimising max(work / waves, row path, sweeps' start + chain), and no mix
-    // whose row blocks hold more than half the waves (their raised waves delay and
-    // slow the sweeps: measured on per-rank shares of C4, N = 4: 20 of 24 aggregates
-    // as row blocks 70 ms per iteration, 7 of 25 58 ms).  Bands and the greedy below
-    // are opt-in (GE_FAML_SYM_BANDED=1): on the same one-GPU rehearsal they were
-    // slower (N = 4 / 8 shares 74 / 49 ms against 57 / 30 ms,
-    // profiles/r04/scale_sim_c4_bands.log).
-    const bool banded_greedy =
-        std::getenv("GE_FAML_SYM_BANDED") && *std::getenv("GE_FAML_SYM_BANDED") == '1';
-    if (chain_k > 0.0 && any_big && force_bands == 0 && !banded_greedy) {
+    std::vector<char> as_rows(big.size(), 0);
+    double best = 0.0;
+    if (chain_k > 0.0 && any_big) {
       std::vector<size_t> by_T(big.size());
       std::iota(by_T.begin(), by_T.end(), 0);
       std::stable_sort(by_T.begin(), by_T.end(), [&](size_t x, size_t y) { return T[x] > T[y]; });
@@ -1110,55 +974,23 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
           row_units += t;
         }
       }
-      const int nopt_rows = sizeof(kOptions) / sizeof(kOptions[0]) - 1;  // kRowsMode
-      for (size_t k = 0; k < best_k; ++k) opt[by_T[k]] = nopt_rows;
+      for (size_t k = 0; k < best_k; ++k) as_rows[by_T[k]] = 1;
       best = pbest;
     }
-    // GE_FAML_SYM_NOBANDS=1 (with the greedy): plain sweeps or whole row blocks only
-    const bool no_bands = std::getenv("GE_FAML_SYM_NOBANDS") && *std::getenv("GE_FAML_SYM_NOBANDS") == '1';
-    if (chain_k > 0.0 && any_big && force_bands == 0 && banded_greedy) {
-      const int nopt = sizeof(kOptions) / sizeof(kOptions[0]);
-      for (;;) {
-        size_t crit = 0;
-        predict(&crit);
-        // sweep pairs have no banded form; bands need 2 tiles each and 14-bit indices
-        int next = opt[crit] + 1;
-        while (next < nopt && kOptions[next] != kRowsMode &&
-               (pl->sym_pair || no_bands || kOptions[next] > T[crit] / 2 ||
-                T[crit] > kUnitMaxTile))
-          ++next;
-        if (next >= nopt) break;
-        const int keep = opt[crit];
-        opt[crit] = next;
-        // equal counts as progress: aggregates of one size tie for the longest chain
-        // and the prediction falls only once every one of them has moved
-        const double p = predict(nullptr);
-        if (p <= best * (1.0 + 1e-12)) {
-          best = std::min(best, p);
-        } else {
-          opt[crit] = keep;
-          break;
-        }
-      }
-    }
     if (std::getenv("GE_FAML_PLAN_DEBUG") && any_big) {
-      int nb = 0, nr = 0;
-      for (size_t b = 0; b < big.size(); ++b) {
-        nb += mode_of(b) != 1 && mode_of(b) != kRowsMode;
-        nr += mode_of(b) == kRowsMode;
-      }
+      int nr = 0;
+      for (size_t b = 0; b < big.size(); ++b) nr += as_rows[b];
       std::fprintf(stderr,
-                   "faml plan: %zu streamed aggregates, T max %d, waves %.0f, %d banded, %d as "
-                   "row blocks, predicted %.1f tile-times\n",
-                   big.size(), *std::max_element(T.begin(), T.end()), waves, nb, nr, best);
+                   "faml plan: %zu streamed aggregates, T max %d, waves %.0f, %d as row blocks, "
+                   "predicted %.1f tile-times\n",
+                   big.size(), *std::max_element(T.begin(), T.end()), waves, nr, best);
     }
-    pl->banded = pl->rows_mode = pl->swept = 0;
+    pl->rows_mode = pl->swept = 0;
     for (size_t b = 0; b < big.size(); ++b) {
-      const int K = mode_of(b);
-      if (K == kRowsMode) ++pl->rows_mode;
-      else if (K == 1 || pl->sym_pair) ++pl->swept;
+      if (as_rows[b]) ++pl->rows_mode;
+      else ++pl->swept;
     }
-    struct Unit { int a, A, pb, T, word; double est; };
+    struct Unit { int a, A, pb, T, kind; double est; };
     std::vector<Unit> us;
     int pb = 0;
     // Queue position of sweep A of an aggregate of T row tiles: 2A Tmax / T, i.e.
@@ -1166,10 +998,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // their last (chain-bound) sweeps together and the launch ends without a tail of
     // the largest aggregate's chain (C4: tail after the queue drained 8.7 -> 3.5 ms,
     // 148.1 -> 143.2 ms per launch).  GE_FAML_SYM_PROP=0: 2A, the sweep's earliest
-    // start (diagnostics; GE_FAML_SYM_EST scales the 2).  In a band [b0, b1) the
-    // sweeps start after the pre blocks (row_k b0) and 2 (A - b0) into the band; a
-    // post block follows its sweep's b1 - A tiles.  Every unit comes after the units
-    // it waits on (pre before sweeps, sweep A - 1 before A, sweep A before post A).
+    // start (diagnostics; GE_FAML_SYM_EST scales the 2).  Every sweep comes after the
+    // sweeps it waits on (sweep A - 1 before A).
     double est_k = 2.0;
     if (const char* e = std::getenv("GE_FAML_SYM_EST")) est_k = std::atof(e);
     const bool est_prop = !(std::getenv("GE_FAML_SYM_PROP") && *std::getenv("GE_FAML_SYM_PROP") == '0');
@@ -1186,172 +1016,34 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     auto scale_of = [&](int Tb) {
       return (est_prop ? (double)Tmax / Tb : 1.0) * (1.0 - big_first * Tb / Tmax);
     };
-    std::vector<Unit> rows_units;
     for (size_t b = 0; b < big.size(); ++b) {
-      const int K = mode_of(b);
-      if (K == kRowsMode) {
-        // whole row blocks by default; GE_FAML_ROWSEG=t cuts them into column segments
-        // of about t tiles, layer g after layer g - 1 in the queue (N = 8 shares of C4:
-        // the tail shrank from 10.4 to 3.6 ms but the launch did not, 33.7 against
-        // 31.5 ms per iteration, profiles/r04/scale_sim_c4_rows_seg.log)
-        int seg = 0;
-        if (const char* e = std::getenv("GE_FAML_ROWSEG")) seg = std::max(0, std::atoi(e));
-        const int G = seg > 0 && T[b] <= kUnitMaxTile ? std::max(1, (T[b] + seg - 1) / seg) : 1;
-        if (G == 1) {
-          for (int A = 0; A < T[b]; ++A)
-            rows_units.push_back({big[b], A, 0, T[b], unit_word(kUnitRows, 0, 0), -1.0});
-        } else {
-          for (int g = 0; g < G; ++g) {
-            const int c0 = (int)((long long)T[b] * g / G), c1 = (int)((long long)T[b] * (g + 1) / G);
-            for (int A = 0; A < T[b]; ++A)
-              rows_units.push_back({big[b], A, pb, T[b], unit_word(kUnitRowSeg, c0, c1),
-                                    -1.0 + 1e-6 * g});
-          }
-          pb += T[b];  // the row tiles' progress counters
-        }
+      if (as_rows[b]) {
+        // row blocks have no dependencies and each spans its aggregate's whole width:
+        // first in the queue, longest first (measured on per-rank shares of C4: N = 4
+        // 69 ms per iteration against 80 ms when spread among the sweeps).  Round 5
+        // tried cutting the last-taken blocks into a head and a tail segment
+        // (McNaughton's wrap-around, so the queue's last round is short): bit-exact,
+        // no faster (N = 8 shares 26.6-28.0 against 27.0-27.3 ms per launch,
+        // profiles/r05/scale_sim_c4_tailsplit.log) -- the share is bound by the row
+        // blocks' instruction stream, not by the queue's last round.
+        for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, 0, T[b], kUnitRows, -1.0});
         continue;
       }
       const double sc = scale_of(T[b]);
-      if (pl->sym_pair) {  // row tiles (A, A + 1); a last odd tile with an inert second
-        for (int A = 0; A < T[b]; A += 2) us.push_back({big[b], A, pb, T[b], 2, est_k * A * sc});
-      } else if (K == 1) {
-        for (int A = 0; A < T[b]; ++A)
-          us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, 0, 0), est_k * A * sc});
-      } else {
-        ++pl->banded;
-        for (int i = 0; i < K; ++i) {
-          const int b0 = band_lo(T[b], K, i), b1 = band_lo(T[b], K, i + 1);
-          const bool last = i + 1 == K;
-          const double e0 = row_k * b0 * sc;  // the band's first sweep
-          for (int A = b0; A < b1; ++A) {
-            // the pre block of tile A is due when the band's first sweep reaches
-            // column tile A; all of the band's pre blocks stay ahead of that sweep
-            // in the queue (a unit waits only on units before it)
-            if (b0 > 0)
-              us.push_back({big[b], A, pb, T[b], unit_word(kUnitPre, b0, b1),
-                            std::min((A - b0) * sc, e0 - 1e-3) - 1e-3});
-            us.push_back({big[b], A, pb, T[b], unit_word(kUnitSweep, b0, last ? 0 : b1),
-                          e0 + est_k * (A - b0) * sc});
-          }
-        }
-      }
+      for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], kUnitSweep, est_k * A * sc});
       pb += T[b];
     }
     for (int a : split) {  // this rank's row tiles of the split aggregates: row blocks
       int t0, t1;
       tiles_of(a, rank, t0, t1);
       const int Ta = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
-      for (int A = t0; A < t1; ++A)
-        rows_units.push_back({a, A, 0, Ta, unit_word(kUnitRows, 0, 0), -1.0});
+      for (int A = t0; A < t1; ++A) us.push_back({a, A, 0, Ta, kUnitRows, -1.0});
     }
-    // Tail split (round 5).  A share of a multi-GPU run that is all row blocks holds
-    // ~2.1 (N = 8) or ~4.2 (N = 4) row blocks of 500-656 tiles per wave, so the
-    // longest-first queue ends with a last round on a few hundred waves: at N = 8 the
-    // queue drained at 17.9 ms and the last block ended at 28.3 ms
-    // (profiles/r04/sym_timeline_rows_n8.json).  A row block's rows add their partners
-    // in order, so it cannot be cut into parallel pieces, but it can be cut in two
-    // consecutive column segments run at different times (McNaughton's wrap-around):
-    // the head (columns [0, 64 h)) at the front of the queue, the tail (the rest,
-    // continuing the rows' sums from F) at its end, where the smaller pieces fill the
-    // waves evenly.  The head is long done when its tail is taken.  Which blocks are
-    // cut (the k smallest) and where (h = f T) is chosen by list-scheduling the queue
-    // on the plan's waves.  Bit-exact (test_faml_tail_split_row_blocks), but measured
-    // no faster (N = 8 shares 26.6-28.0 against 27.0-27.3 ms per launch,
-    // profiles/r05/scale_sim_c4_tailsplit.log): the share is bound by the row blocks'
-    // instruction stream, not by the queue's last round -- opt-in GE_FAML_TAILSPLIT=1
-    // (GE_FAML_TAILSPLIT_K / _F force the cut for tests).
-    pl->tail_split = 0;
-    {
-      const char* e = std::getenv("GE_FAML_TAILSPLIT");
-      const bool on = (e && *e == '1') || std::getenv("GE_FAML_TAILSPLIT_K");
-      bool all_rows = on && !rows_units.empty() && std::getenv("GE_FAML_ROWSEG") == nullptr;
-      all_rows = all_rows && us.empty();  // sweeps present: not a rows-only share
-      for (const Unit& x : rows_units) all_rows = all_rows && (x.word & 15) == kUnitRows && x.T >= 4;
-      if (all_rows) {
-        std::stable_sort(rows_units.begin(), rows_units.end(),
-                         [](const Unit& x, const Unit& y) { return x.T > y.T; });
-        const int m = std::max(1, (int)waves);
-        const size_t nu = rows_units.size();
-        double seg_cost = 1.0;  // tile-times per extra segment (F hand-over, restart)
-        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_COST")) seg_cost = std::atof(s);
-        // list schedule of the queue: heads of the k last blocks, whole blocks, tails
-        auto simulate = [&](size_t k, double f) {
-          std::priority_queue<double, std::vector<double>, std::greater<double>> freeq;
-          for (int w = 0; w < m; ++w) freeq.push(0.0);
-          std::vector<double> head_end(nu, 0.0);
-          auto take = [&](double dur, double ready) {
-            const double t0 = std::max(freeq.top(), ready);
-            freeq.pop();
-            freeq.push(t0 + dur);
-            return t0 + dur;
-          };
-          double span = 0.0;
-          for (size_t i = nu - k; i < nu; ++i) {
-            const int T = rows_units[i].T, h = std::min(T - 1, std::max(1, (int)std::lround(f * T)));
-            head_end[i] = take(h + seg_cost, 0.0);
-          }
-          for (size_t i = 0; i < nu - k; ++i) span = std::max(span, take(rows_units[i].T, 0.0));
-          for (size_t i = nu - k; i < nu; ++i) {
-            const int T = rows_units[i].T, h = std::min(T - 1, std::max(1, (int)std::lround(f * T)));
-            span = std::max(span, take(T - h + seg_cost, head_end[i]));
-          }
-          return span;
-        };
-        double best_span = simulate(0, 0.5), best_f = 0.5;
-        size_t best_k = 0;
-        const size_t step = std::max<size_t>(1, nu / 128);
-        for (double f : {0.5, 0.6, 0.7, 0.8, 0.9})
-          for (size_t k = step; k <= nu; k += step) {
-            const double sp = simulate(k, f);
-            if (sp < best_span * 0.999) {
-              best_span = sp;
-              best_k = k;
-              best_f = f;
-            }
-          }
-        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_K")) best_k = std::min(nu, (size_t)std::atol(s));
-        if (const char* s = std::getenv("GE_FAML_TAILSPLIT_F")) best_f = std::atof(s);
-        if (best_k > 0 && std::getenv("GE_FAML_PLAN_DEBUG"))
-          std::fprintf(stderr,
-                       "faml plan: tail split of %zu of %zu row blocks at %.2f, predicted %.0f "
-                       "tile-times (whole %.0f)\n",
-                       best_k, nu, best_f, best_span, simulate(0, 0.5));
-        std::map<int, int> pbase;  // progress counters of the aggregates with split blocks
-        for (size_t i = nu - best_k; i < nu; ++i) {
-          Unit& x = rows_units[i];
-          auto it = pbase.find(x.a);
-          if (it == pbase.end()) {
-            it = pbase.emplace(x.a, pb).first;
-            pb += x.T;
-          }
-          const int h = std::min(x.T - 1, std::max(1, (int)std::lround(best_f * x.T)));
-          Unit head = x;
-          head.pb = it->second;
-          head.word = unit_word(kUnitRowSeg, 0, h);
-          head.est = -3.0;
-          x.pb = it->second;
-          x.word = unit_word(kUnitRowSeg, h, x.T);
-          x.est = -1.0;
-          us.push_back(head);
-        }
-        for (size_t i = 0; i < nu - best_k; ++i) rows_units[i].est = -2.0;
-        pl->tail_split = (int)best_k;
-      }
-    }
-    // row blocks have no dependencies and each spans its aggregate's whole width (or
-    // the members before a band): first in the queue (measured on per-rank shares of
-    // C4: N = 4 69 ms per iteration against 80 ms when spread among the sweeps)
-    for (size_t k = 0; k < rows_units.size(); ++k) us.push_back(rows_units[k]);
     std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
       return x.est != y.est ? x.est < y.est : x.T > y.T;
     });
     std::vector<int4> h_units;
-    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.word));
-    pl->sym_ext = false;
-    for (const Unit& x : us) {
-      const int kind = x.word & 15, b1 = (x.word >> 18) & kUnitMaxTile;
-      pl->sym_ext = pl->sym_ext || kind == kUnitPre || kind == kUnitRowSeg || (kind == 0 && b1 > 0);
-    }
+    for (const Unit& x : us) h_units.push_back(make_int4(x.a, x.A, x.pb, x.kind));
     pl->nunits = (int)h_units.size();
     pl->ntiles = pb;
     pl->units.alloc(h_units.size());
@@ -1498,11 +1190,6 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                            pl->beg.p, pl->pt_ip, pl->pt_ix, pl->pos.p, pl->vA, pl->ip, pl->ix,
                            pl->dx, cA, rA, init, pl->Fscr.p, pl->Fprev.p, X, iters, c);
     };
-    // GE_FAML_RESIDENT_FIRST=1: the resident classes are queued before the streamed
-    // path (tuning: their overlap with the first repulsion launches)
-    const bool resident_first =
-        std::getenv("GE_FAML_RESIDENT_FIRST") && *std::getenv("GE_FAML_RESIDENT_FIRST") == '1';
-    if (resident_first) launch_resident();
     // streamed path (side[0])
     hipStream_t ss = pl->side[0];
     if (ev) GE_HIP(hipEventRecord(ev[2], ss));
@@ -1511,10 +1198,6 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
       hipLaunchKernelGGL((faml_huge_init<D>), dim3((nr + kHT - 1) / kHT), dim3(kHT), 0, ss,
                          nr, pl->irows.p, init, pl->Xa.p, pl->Fprev.p);
       GE_HIP(hipMemsetAsync(pl->queue.p, 0, sizeof(int) * iters, ss));
-      if (pl->pull.p && pl->nrows > 0)  // cA is fixed for the whole call
-        hipLaunchKernelGGL((pull_precompute_kernel<D>), dim3((pl->nrows + 3) / 4), dim3(256), 0,
-                           ss, pl->nrows, pl->rows.p, pl->pt_ix, pl->ip, pl->ecode.p, pl->vA, cA,
-                           pl->pull.p);
       double* cur = pl->Xa.p;
       double* nxt = pl->Xb.p;
       for (int it = 0; it < iters; ++it) {
@@ -1531,53 +1214,34 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           GE_HIP(hipEventRecord(re[0], ss));
         }
         const FamlRows<D> fr{pl->pt_ip, pl->pt_ix, pl->ecode.p, pl->ip, pl->vA, pl->dx,
-                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c, pl->pull.p};
-        // the heavy member rows' segment terms need only `cur`: queued beside the
-        // repulsion launch (ge_rows.hpp launch_rows_early)
-        const bool rows_early =
-            pl->nrows > 0 && launch_rows_early<D>(pl->ecls, fr, ss, pl->rstreams);
+                             cA, cur, pl->DP.p, pl->Fscr.p, nxt, pl->Fprev.p, c};
         if (pl->sym) {
           if (pl->ntiles) GE_HIP(hipMemsetAsync(pl->prog.p, 0, sizeof(int) * pl->ntiles, ss));
-          // GE_SYM_HAND_F=1: hand-overs through F's records (round-3 layout; A/B only)
-          const bool hand_f = std::getenv("GE_SYM_HAND_F") && *std::getenv("GE_SYM_HAND_F") == '1';
-          double* H = hand_f ? pl->Fscr.p : pl->hand.p;
-          const size_t hs = hand_f ? 0 : (size_t)pl->n;
+          double* H = pl->hand.p;  // hand-overs component-major (ge_sym.hpp sym_handover)
+          const size_t hs = (size_t)pl->n;
           int* err = pl->sym_err.p;
           const long long lim = pl->sym_limit;
-          if (pl->sym_pair) {
-            if (!pl->stamp_path.empty())
-              hipLaunchKernelGGL((faml_sym_pair<D, false, true>), dim3(pl->sym_blocks), dim3(64),
-                                 0, ss, pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim,
-                                 pl->stamps.p);
-            else if (c.repel == 1.0)
-              hipLaunchKernelGGL((faml_sym_pair<D, true>), dim3(pl->sym_blocks), dim3(64), 0, ss,
-                                 pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim, nullptr);
-            else
-              hipLaunchKernelGGL((faml_sym_pair<D, false>), dim3(pl->sym_blocks), dim3(64), 0, ss,
-                                 pl->nunits, pl->units.p, pl->queue.p + it, pl->pt_ip, cur,
-                                 pl->DP.p, c.repel, pl->Fscr.p, pl->prog.p, err, lim, nullptr);
+          if (false) {
 #ifdef GE_SYM_DIAGNOSTICS
           } else if (!pl->stamp_path.empty() && std::getenv("GE_SYM_NOWAIT")) {
             // timing only, WRONG results: no sweep waits for its hand-overs.  Built
             // only with -DGE_SYM_DIAGNOSTICS (scripts/build_variant.sh NAME -DGE_SYM_DIAGNOSTICS), never in the
             // shipped library.
             std::fprintf(stderr, "libge: GE_SYM_NOWAIT diagnostics build: results are invalid\n");
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true, true>), dim3(pl->sym_blocks),
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);
 #endif
           } else if (!pl->stamp_path.empty()) {
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false, true>), dim3(pl->sym_blocks),
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);
           } else {
             sym_repulse_launch(D, pl->sym_blocks, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim, pl->sym_ext);
+                               err, lim);
           }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
@@ -1596,7 +1260,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           pl->next_aev += 2;
           GE_HIP(hipEventRecord(ae[0], ss));
         }
-        if (pl->nrows > 0) launch_rows<D>(pl->ecls, fr, ss, pl->rstreams, rows_early);
+        if (pl->nrows > 0) launch_rows<D>(pl->ecls, fr, ss, pl->rstreams);
         if (ae) GE_HIP(hipEventRecord(ae[1], ss));
         if (pl->xwidth > 0)  // every rank's rows of the split aggregates, for the next step
           exchange_rows(pl->comm, ss, D, pl->xrows.p, pl->xcounts.p, pl->xfirst.p,
@@ -1607,15 +1271,10 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                          pl->pt_ip, pl->pt_ix, cur, cA, rA, X);
     }
     if (ev) GE_HIP(hipEventRecord(ev[3], ss));
-    // GE_FAML_RESIDENT_SERIAL=1 (tuning): the resident classes only after the streamed
-    // path, not beside it
-    if (std::getenv("GE_FAML_RESIDENT_SERIAL") && *std::getenv("GE_FAML_RESIDENT_SERIAL") == '1' &&
-        !resident_first) {
-      GE_HIP(hipEventRecord(pl->join[0], ss));
-      for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(pl->side[k], pl->join[0], 0));
-      GE_HIP(hipStreamWaitEvent(st, pl->join[0], 0));
-    }
-    if (!resident_first) launch_resident();
+    // the resident classes beside the streamed path: queued after it, they cost the
+    // repulsion launch ~0.3 ms; run after it, ~1.4 ms per step; queued before it,
+    // nothing changes (profiles/r04/ab_launch_order.log)
+    launch_resident();
     for (int k = 0; k < 3; ++k) GE_HIP(hipEventRecord(pl->join[k], pl->side[k]));
     for (int k = 1; k < 3; ++k) GE_HIP(hipStreamWaitEvent(st, pl->join[k], 0));
     if (ev) GE_HIP(hipEventRecord(ev[1], st));  // resident classes done
@@ -1637,7 +1296,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
     GE_HIP(hipStreamSynchronize(st));
     GE_HIP(hipMemcpy(h.data(), pl->stamps.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
     if (FILE* f = std::fopen(pl->stamp_path.c_str(), "wb")) {
-      const int hdr[4] = {pl->nunits, kStampWords, pl->sym_blocks, pl->sym_pair ? 64 : kSymT};
+      const int hdr[4] = {pl->nunits, kStampWords, pl->sym_blocks, kSymT};
       std::fwrite(hdr, sizeof(int), 4, f);
       std::fwrite(pl->h_units.data(), sizeof(int4), pl->h_units.size(), f);
       std::fwrite(h.data(), sizeof(long long), h.size(), f);
@@ -1649,25 +1308,15 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
                         double repel, double* F, double* H, size_t hs, int* prog, int* err,
-                        long long limit, bool ext) {
+                        long long limit) {
   dispatch_dim(dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    if (ext) {  // band / segmented-row units present
-      if (repel == 1.0)
-        hipLaunchKernelGGL((faml_sym_repulse<D, true, false, false, true>), dim3(blocks),
-                           dim3(kSymT), 0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs,
-                           prog, err, limit, nullptr);
-      else
-        hipLaunchKernelGGL((faml_sym_repulse<D, false, false, false, true>), dim3(blocks),
-                           dim3(kSymT), 0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs,
-                           prog, err, limit, nullptr);
-    } else if (repel == 1.0) {
+    if (repel == 1.0)
       hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(blocks), dim3(kSymT), 0, s, nunits,
                          units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
-    } else {
+    else
       hipLaunchKernelGGL((faml_sym_repulse<D, false>), dim3(blocks), dim3(kSymT), 0, s, nunits,
                          units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
-    }
   });
   GE_HIP(hipGetLastError());
 }
@@ -1930,7 +1579,7 @@ int ge_faml_plan_schedule(ge_faml_plan* pl, int* sweeps, int* banded, int* row_b
   return ge::guarded([&] {
     GE_REQUIRE(pl && sweeps && banded && row_blocks && units, "null argument");
     *sweeps = pl->swept;
-    *banded = pl->banded;
+    *banded = 0;  // bands were removed in round 5 (the ABI keeps the field)
     *row_blocks = pl->rows_mode;
     *units = pl->nunits;
   });

@@ -64,7 +64,6 @@ struct RowClasses {
   const long long* hoff = nullptr;
   int seg_mode = 0;               // kSegBinade / kSegStore when nseg > 0
   int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0, nseg = 0;
-  int xcd = 1;       // tile_rows_kernel deals tiles XCD-major (xcd_major; GE_ROWS_XCD=0: off)
   int tile_off = 0;  // where tile_ptr starts in the host array
   int seg_off = 0;   // where seg starts in the host array
   int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
@@ -91,8 +90,6 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
                           std::vector<int>* heavy_deg = nullptr) {
   bool tiles = ids.size() >= (size_t)kTileMinRows;
   if (const char* e = std::getenv("GE_ROWS_TILES")) tiles = std::atoi(e) != 0;
-  rc.xcd = 1;
-  if (const char* e = std::getenv("GE_ROWS_XCD")) rc.xcd = std::atoi(e) != 0;
   // few rows (a small level): latency, not throughput -- rows of more than 4
   // entries take a wave (n = 536: attraction 26 -> 13 us per iteration)
   int med = ids.size() <= 65536 ? 4 : kMedDeg, heavy = tiles ? kTileCap : kHeavyDeg;
@@ -625,23 +622,11 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p) {
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
 // Block b + first: a tile (< ntiles) or a heavy-row segment after them; `first`
 // lets the segments run as their own launch (kSegStore, beside the tiles).
-//
-// XCD-aware order (round 5): blocks are dealt round-robin over the 8 XCDs (blocks b
-// and b + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so with block b =
-// tile b every XCD's L2 sees every tile's gathers.  Block b takes tile
-// xcd_major(b) instead: the blocks of one XCD walk one contiguous eighth of the tile
-// list in dispatch order, so the rows whose neighbours sit close together (the
-// members of one aggregate, stored together) are gathered through one L2.
-// GE_ROWS_XCD=0 keeps b (A/B; the host passes xcd = 0).
-__device__ __forceinline__ int xcd_major(int b, int n) {
-  const int q = n >> 3, r = n & 7, x = b & 7;
-  return x * q + min(x, r) + (b >> 3);
-}
 
 template <int D, class P>
 __global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int first = 0) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
-  const int b = (L.xcd ? xcd_major((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x) + first;
+  const int b = (int)blockIdx.x + first;
   if (b < L.ntiles)
     tile_rows<D>(L, p, b, lds);
   else if (L.seg_mode == kSegStore)
@@ -746,56 +731,24 @@ struct RowStreams {
       (void)hipStreamDestroy(side);
     }
     if (fork) (void)hipEventDestroy(fork);
-    if (mid) (void)hipEventDestroy(mid);
     if (join) (void)hipEventDestroy(join);
   }
   void ensure() {
     if (side) return;
-    // GE_ROWS_SIDE_PRIO=1: the side stream (heavy segments + chains, the pass's
-    // longer branch) at the device's highest stream priority (tuning)
-    const char* e = std::getenv("GE_ROWS_SIDE_PRIO");
-    if (e && *e == '1') {
-      int least = 0, greatest = 0;
-      GE_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      GE_HIP(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, greatest));
-    } else {
-      GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    }
+    GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     GE_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-    GE_HIP(hipEventCreateWithFlags(&mid, hipEventDisableTiming));
     GE_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
   }
-  hipEvent_t mid = nullptr;  // launch_rows after launch_rows_early: the sums are ready
 };
 
-// kSegStore with tiles: the heavy rows' segment terms depend on the coordinates
-// only, not on the accumulators' start values (the repulsion sums).  Called before
-// the launch that writes those sums (the streamed repulsion), this queues the
-// segments on rs.side at once, so they run beside that launch; the matching
-// launch_rows(..., early = true) then queues only the chains and the tiles.
-// Returns whether it did.  Opt-in (GE_ROWS_EARLY=1): bit-exact, and the C4 pass
-// fell from 3.54 to 2.2-2.4 ms, but the repulsion launch beside it rose from 136.3
-// to 141-142 ms (140.6 against 144-145 ms per step, profiles/r04/ab_rows_early.log).
-template <int D, class P>
-inline bool launch_rows_early(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
-  if (!(rc.nseg > 0 && rc.seg_mode == kSegStore && rc.ntiles > 0) || std::getenv("GE_ROWS_SERIAL"))
-    return false;
-  const char* e = std::getenv("GE_ROWS_EARLY");
-  if (!(e && *e == '1')) return false;
-  rs.ensure();
-  GE_HIP(hipEventRecord(rs.fork, s));
-  GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
-  hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
-                     rc.ntiles);
-  return true;
-}
-
 // All rows of `rc` on stream s (the heavy ones on rs.side when there are tiles;
-// s waits for them before returning to the caller's next work).  early: the
-// segments were queued by launch_rows_early with the same arguments.
+// s waits for them before returning to the caller's next work).  Round 4 also
+// queued the heavy rows' segment terms beside the multilevel repulsion launch
+// (they need only the coordinates): bit-exact, the pass fell from 3.54 to 2.2-2.4 ms
+// but the repulsion launch beside it rose from 136.3 to 141-142 ms
+// (profiles/r04/ab_rows_early.log); removed in round 5.
 template <int D, class P>
-inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs,
-                        bool early = false) {
+inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStreams& rs) {
   const int tgrid = rc.ntiles + rc.nseg;
   if (rc.nseg > 0 && rc.seg_mode == kSegStore && rc.ntiles > 0 &&
       !std::getenv("GE_ROWS_SERIAL")) {
@@ -803,15 +756,10 @@ inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStre
     // dependent add per term) is independent of the tiles: segments + chains on the
     // side stream, beside the tiles (C4: 2.16 + 1.43 ms one after the other)
     rs.ensure();
-    if (early) {  // the chains also wait for the sums written on s
-      GE_HIP(hipEventRecord(rs.mid, s));
-      GE_HIP(hipStreamWaitEvent(rs.side, rs.mid, 0));
-    } else {
-      GE_HIP(hipEventRecord(rs.fork, s));
-      GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
-      hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
-                         rc.ntiles);
-    }
+    GE_HIP(hipEventRecord(rs.fork, s));
+    GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
+                       rc.ntiles);
     hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy), dim3(64), 0, rs.side, rc, p);
     hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles), dim3(kRowT), 0, s, rc, p, 0);
     GE_HIP(hipEventRecord(rs.join, rs.side));

@@ -1,11 +1,14 @@
 // ge_selftest.hip -- on-device check of the exact shared-reciprocal division
 // (ge_math.hpp): for operands in the domain the strict kernels admit, div_by
-// must return the same bits as the compiler's IEEE `/`.
+// must return the same bits as the compiler's IEEE `/`; and the repulsion term
+// with pair_den's rcp-free reciprocals (ge_pair.hpp) the same bits as with
+// recip_of's and as the `/` form.
 
 #include <hip/hip_runtime.h>
 
 #include "ge_internal.hpp"
 #include "ge_math.hpp"
+#include "ge_pair.hpp"
 
 namespace ge {
 namespace {
@@ -79,6 +82,41 @@ __global__ void selftest_kernel(long long samples, unsigned long long seed,
     const double cij = rnd_exp(h2 ^ h1, -180, 180, false);
     const double dd = den * den;
     if (!same(div_by(cij, dd, recip_of(dd)), cij / dd)) ++fails;
+    // a repulsion pair (ge_pair.hpp rep_term): pair_den's reciprocals against
+    // recip_of's and against `/`.  Coordinates mostly of the layout's scale, some
+    // spread over the whole domain, some pairs at or below the eps clamp, and
+    // coincident ones; deg+1 and repel over their domain.
+    const unsigned long long h4 = mix(h3), h5 = mix(h4), h6 = mix(h5), h7 = mix(h6);
+    double xi[3], xj[3];
+    const unsigned shape = (unsigned)(h4 & 7);
+    const double scale = shape < 4 ? 1.0 : rnd_exp(h7, -190, 190, false);
+    for (int k = 0; k < 3; ++k) {
+      const unsigned long long hk = mix(h5 + k);
+      xi[k] = ((double)(hk >> 11) * 0x1.0p-53 * 2.0 - 1.0) * scale;
+      if (!coord_ok(xi[k])) xi[k] = 0.0;
+      const unsigned long long hj = mix(h6 + k);
+      double off = ((double)(hj >> 11) * 0x1.0p-53 * 2.0 - 1.0) * scale;
+      if (shape == 1) off = off * 1e-5;                 // near the eps clamp
+      if (shape == 2) off = rnd_exp(hj, -30, -10, true);  // around eps
+      if (shape == 3) off = 0.0;                        // coincident
+      xj[k] = xi[k] + off;
+      if (!coord_ok(xj[k])) xj[k] = xi[k];
+    }
+    const double di = (h7 & 1) ? 1.0 + (double)((h7 >> 8) & 1023) : rnd_exp(h7, -60, 59, false);
+    const double dj = (h6 & 1) ? 1.0 + (double)((h6 >> 8) & 1023) : rnd_exp(h6, -60, 59, false);
+    const double rp = (h5 & 3) ? 1.0 : rnd_exp(h5 ^ h7, -60, 0, false);
+    if (!(vertex_ok<3>(xi, di) && vertex_ok<3>(xj, dj) && weight_ok(rp) &&
+          weight_ok(di * dj * rp)))
+      continue;
+    double ta[3], tb[3], tc[3];
+    rep_term<3, true, false>(xi, xj, di, dj, rp, ta);
+    rep_term_rcp<3, false>(xi, xj, di, dj, rp, tb);
+    rep_term<3, false, false>(xi, xj, di, dj, rp, tc);
+    for (int k = 0; k < 3; ++k) {
+      // +-0 terms may differ in sign from `/` (div_by_nz); they never change a sum
+      if (!same(ta[k], tb[k])) ++fails;
+      if (!same(ta[k], tc[k]) && !(ta[k] == 0.0 && tc[k] == 0.0)) ++fails;
+    }
   }
   if (fails) atomicAdd(bad, fails);
 }

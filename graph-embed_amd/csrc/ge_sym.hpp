@@ -150,11 +150,10 @@ __device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, c
   }
 }
 
-// Hand-over slot of member c, dimension k: component-major H[k * hs + c], or with
-// hs == 0 record-major H[c * D + k] (H = F, the round-3 layout; GE_SYM_HAND_F=1, A/B)
+// Hand-over slot of member c, dimension k: component-major H[k * hs + c].
 template <int D>
 __device__ __forceinline__ double* hand_at(double* H, size_t hs, size_t c, int k) {
-  return hs ? H + k * hs + c : H + c * D + k;
+  return H + k * hs + c;
 }
 
 // Column tile t of the sweep has left lane 63: write its sums back, then let the
@@ -328,12 +327,10 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
                                            double* __restrict__ H, size_t hs, int* err,
                                            long long limit, bool& give_up, double* rec,
                                            double* ini, double* out, long long& spin,
-                                           long long& t_first, int cend,
-                                           double (&rout)[D]) {
+                                           long long& t_first, double (&rout)[D]) {
   constexpr int IW = SymI<D>::v;
   const size_t cbase = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
-  if (cend <= 0 || cend > s) cend = s;  // a band's sweeps stop at the band's end
   double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
 #pragma unroll
   for (int k = 0; k < D; ++k) {
@@ -343,7 +340,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   }
   if (rv) dr = DP[cbase + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
-  const int ncols = cend - 64 * A;
+  const int ncols = s - 64 * A;
   const int ntiles = (ncols + 63) >> 6;
   bool ok_prev = true;
   for (int tt = 0; tt < ntiles; ++tt) {
@@ -406,8 +403,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
                                        xr, dr, rv, repel, racc, flow);
   if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
-  // the rows' sums: the caller writes them to F, or (a band before the last)
-  // continues them with the members after the band
+  // the rows' sums: the caller writes them to F
 #pragma unroll
   for (int k = 0; k < D; ++k) rout[k] = racc[k];
 }
@@ -424,51 +420,26 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
   w[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
 }
 
-// Banded aggregates.  A sweep chain is ~2.5 T tile-times however many CUs are
-// idle (each sweep starts ~2 tiles behind the one before), which bounds a share
-// of a multi-GPU run.  An aggregate cut into K bands of row tiles
-// [b0, b1) keeps the reference's per-row order as three parts per row:
-//   pre   (kind 3): the band's rows against the members before the band, as a row
-//         block; those sums are exactly the entering column sums of the band's
-//         first sweep, so they go to H and the band's tiles' progress counters
-//         are set to b0;
-//   sweeps (kind 0, band end b1): the band's rows and columns symmetric, each row
-//         continuing from its column sum at the diagonal as before;
-//   post: the same wave, once its band sweep is done, continues its rows against
-//         the members after the band as a row block (the row sums stay in
-//         registers; the sweep's hand-overs all happened in the band part).
-// The chain of band b is ~0.8 b0 + 2.5 (b1 - b0) + 0.8 (T - b1) tile-times; the
-// cross-band pairs are evaluated twice (ordered), the in-band pairs once.
-// Segmented row blocks (kind 5, opt-in GE_FAML_ROWSEG): a row tile's row block cut
-// into column segments [c0, c1) of tiles, run as separate units in layers (every
-// row tile's first segment, then every second, ...); a segment continues the rows'
-// sums of the one before (F, agent scope; progress counter = the segment's first
-// column tile).  A whole row block is T tiles of one wave and the last ones taken
-// set the launch's tail (N = 8 share of C4: queue drained at 17.9 ms, last block
-// ended at 28.3 ms); segments cut the tail to 3.6 ms but not the launch
-// (profiles/r04/sym_timeline_*_n8.json).
-constexpr int kUnitSweep = 0, kUnitRows = 1, kUnitPre = 3, kUnitRowSeg = 5;
-__host__ __device__ inline int unit_word(int kind, int b0, int b1) {
-  return kind | (b0 << 4) | (b1 << 18);
-}
-constexpr int kUnitMaxTile = (1 << 14) - 1;  // band tile indices are 14-bit fields
+// Unit kinds: a symmetric sweep, or a whole row block (an aggregate whose sweep
+// chain would outlast the launch: a share of a multi-GPU run).  Rounds 3-4 also
+// built, bit-exact and measured slower (removed in round 5): pair
+// sweeps (two row tiles per wave), banded aggregates (pre row blocks, in-band sweeps,
+// post row blocks), segmented row blocks and their round-5 tail split.
+constexpr int kUnitSweep = 0, kUnitRows = 1;
 
-// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog,
-// unit_word(kind, band first tile, band end tile)} in queue order; prog (ptiles
-// progress counters) zeroed before the launch; queue = one counter.  Every unit
-// waits only on units before it in the queue.
+// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog, kind}
+// in queue order; prog (ptiles progress counters) zeroed before the launch; queue =
+// one counter.  Every unit waits only on units before it in the queue.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
 // (diagnostics, wrong results): no sweep waits for its hand-overs.
-// EXT: the band and segmented-row unit kinds (kinds 3 and 5, band ends of sweeps).
-// The plain kernel (sweeps and whole row blocks only) stays at <= 120 VGPRs: three
-// of its waves per SIMD (the plan's three blocks per CU) then leave 152 of the 512
-// registers, room for one wave of the resident classes' kernels (143 VGPRs) on the
-// other streams.  With the extra kinds compiled in (or the give-up store inside the
-// wait loop) it took 122-128, the resident kernels were locked out until the
-// repulsion launches ended and ran during the attraction passes instead (C4: 4.44
-// against 3.52 ms per pass, 140.4 against 137.0-137.3 ms per step, the round-3
-// library 138.7-138.9 on the same box; profiles/r04/ab_rows_r03.log).
-template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false, bool EXT = false>
+// The kernel stays at <= 120 VGPRs: three of its waves per SIMD (the plan's three
+// blocks per CU) then leave 152 of the 512 registers, room for one wave of the
+// resident classes' kernels (143 VGPRs) on the other streams.  At 122-128 (with the
+// round-4 band kinds compiled in, or the give-up store inside the wait loop) the
+// resident kernels were locked out until the repulsion launches ended and ran
+// during the attraction passes instead (C4: 4.44 against 3.52 ms per pass, 140.4
+// against 137.0-137.3 ms per step; profiles/r04/ab_rows_r03.log).
+template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
 __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
@@ -498,316 +469,22 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const int A = u.y;
     const int base = pt_ip[u.x];
     const int s = pt_ip[u.x + 1] - base;
-    const int kind = u.w & 15, b0 = (u.w >> 4) & kUnitMaxTile, b1 = (u.w >> 18) & kUnitMaxTile;
     const size_t rb = (size_t)base + 64 * (size_t)A;
-    if (kind == kUnitRows) {
+    if (u.w == kUnitRows) {
       // a row block spans its aggregate's whole width: the launch's critical path
       // when the aggregate is large, so its wave takes issue priority on the SIMD
       __builtin_amdgcn_s_setprio(3);
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
       __builtin_amdgcn_s_setprio(0);
-    } else if (EXT && kind == kUnitRowSeg) {  // columns [64 b0, 64 b1) of row tile A's row block
-      const bool first = b0 == 0, last = 64 * b1 >= s;
-      double acc[D];
-      if (!first) {  // the segment before has stored the rows' sums
-        handover_wait<false>(prog + u.z + A, b0, err, limit, give_up);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-          acc[k] = 64 * A + lane < s ? agent_ld(F + (rb + lane) * D + k) : 0.0;
-      }
-      __builtin_amdgcn_s_setprio(3);
-      rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b0, min(64 * b1, s), first, X, DP, repel,
-                               repel_ok, rec, acc);
-      __builtin_amdgcn_s_setprio(0);
-      if (64 * A + lane < s) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-          if (last) F[(rb + lane) * D + k] = acc[k];
-          else agent_st(F + (rb + lane) * D + k, acc[k]);
-        }
-      }
-      if (!last) {
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_waitcnt(0);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0)
-          __hip_atomic_store(prog + u.z + A, b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (EXT && kind == kUnitPre) {  // entering column sums of band [b0, b1)'s first sweep
-      __builtin_amdgcn_s_setprio(3);
-      double acc[D];
-      rows_range<D, REPEL_ONE>(lane, base, s, A, 0, 64 * b0, true, X, DP, repel, repel_ok, rec,
-                               acc);
-      __builtin_amdgcn_s_setprio(0);
-      if (64 * A + lane < s) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, rb + lane, k), acc[k]);
-      }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_waitcnt(0);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (lane == 0)
-        __hip_atomic_store(prog + u.z + A, b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      // a sweep; in a band that is not the aggregate's last it stops at the band's
-      // end and the same wave continues its rows past the band (post)
-      const bool banded = EXT && b1 > 0 && 64 * b1 < s;
+    } else {  // a sweep
       double racc[D];
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, ini,
-                                              out, spin, t_first, banded ? 64 * b1 : 0, racc);
-      if (banded) {
-        wave_lds_sync();  // the rings are free: the row block stages its tiles in rec
-        rows_range<D, REPEL_ONE>(lane, base, s, A, 64 * b1, s, false, X, DP, repel, repel_ok,
-                                 rec, racc);
-      }
+                                              out, spin, t_first, racc);
       if (64 * A + lane < s) {
 #pragma unroll
         for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = racc[k];
       }
-    }
-    if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
-    wave_lds_sync();
-  }
-  report_give_up(give_up, lane, err);
-}
-
-// ---------------------------------------------------------------------------
-// Pair sweeps (faml_sym_pair): one wave carries the sweeps of row tiles A and
-// A+1 as two systolic streams.  Stream b runs 128 steps behind stream a, so the
-// sum of column q leaves a's lane 63 exactly one step before it has to enter b's
-// lane 0 (a wave rotate moves it there); b's lane 63 stores each finished column
-// sum to F.  Per column, rows of tile A then rows of tile A+1 in ascending order:
-// the order of two consecutive single sweeps, so the same bits.  The two streams
-// are independent instruction chains (twice the work between waits), the column
-// records are staged once for both, and only every second row tile hands its
-// column tiles over.  An aggregate with an odd tile count ends with a pair whose
-// stream b rows are all past the aggregate (inert: its terms are +-0).
-//
-// Stream a at step tau, lane l: (row 64A + l, column tau - l); stream b: (row
-// 64(A+1) + l, column tau - 64 - l) (columns relative to 64A).  Records: a ring
-// of four column tiles (stream a reads tiles tt-1 and tt during global tile tt,
-// stream b tiles tt-2 and tt-1).  Column C leaves stream b at step C + 127, so
-// column tile K is complete after global tile K + 2 (K >= 2: tiles 0 and 1 are
-// the pair's own rows).  LDS: 9.5 KB per wave at D = 3 (four waves per SIMD).
-
-constexpr int kPairRec = 256;  // record slots per component (4 column tiles)
-constexpr int kPairIni = 64;   // entering column sums of stream a (the current tile)
-
-template <int D>
-constexpr int pair_arena_doubles() {
-  const int pair = (D + 1) * kPairRec + kPairIni * SymI<D>::v;
-  const int rows = 64 * SymW<D>::v;
-  return pair > rows ? pair : rows;
-}
-
-// Wave rotate by one lane (DPP wave_ror:1): lane l receives lane l-1, lane 0 lane 63.
-__device__ __forceinline__ double wave_ror1(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x13C, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x13C, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// STORE: b's lane 63 stores the column leaving it (tau >= 255, i.e. columns >= 128).
-template <int D, bool SHARED, bool REPEL_ONE, bool DIAG_A, bool DIAG_B, bool STORE>
-__device__ __forceinline__ void pair_step(int tau, int lane, const double* rec, const double* ini,
-                                          double* Fc, const double (&xa)[D], double da,
-                                          const double (&xb)[D], double db, double repel,
-                                          double (&racc_a)[D], double (&flow_a)[D],
-                                          double (&racc_b)[D], double (&flow_b)[D]) {
-  constexpr int IW = SymI<D>::v;
-  const double* ic = ini + (tau & (kPairIni - 1)) * IW;
-  const int sa = (tau - lane) & (kPairRec - 1);
-  const int sb = (tau - 64 - lane) & (kPairRec - 1);
-  double ia[D], ra[D + 1], rb[D + 1];
-#pragma unroll
-  for (int k = 0; k < D; ++k) ia[k] = ic[k];
-#pragma unroll
-  for (int k = 0; k <= D; ++k) {
-    ra[k] = rec[k * kPairRec + sa];
-    rb[k] = rec[k * kPairRec + sb];
-  }
-  // b's entering column is the sum that left a's lane 63 at the previous step;
-  // column tau enters a's lane 0 with its stored sum
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    flow_b[k] = wave_ror1(lane == 63 ? flow_a[k] : flow_b[k]);
-    flow_a[k] = wave_shift_in(flow_a[k], ia[k]);
-  }
-  const bool diag_a = DIAG_A && tau - lane == lane;
-  const bool diag_b = DIAG_B && tau - 128 - lane == lane;
-  if (diag_a)
-#pragma unroll
-    for (int k = 0; k < D; ++k) racc_a[k] = flow_a[k];
-  if (diag_b)
-#pragma unroll
-    for (int k = 0; k < D; ++k) racc_b[k] = flow_b[k];
-  double ta[D], tb[D];
-  rep_term<D, SHARED, REPEL_ONE>(xa, ra, da, ra[D], repel, ta);
-  rep_term<D, SHARED, REPEL_ONE>(xb, rb, db, rb[D], repel, tb);
-  if (!SHARED && (diag_a || diag_b)) {  // the `/` form skips the self pair (ge_pair.hpp)
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      if (diag_a) ta[k] = 0.0;
-      if (diag_b) tb[k] = 0.0;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    racc_a[k] = racc_a[k] + ta[k];
-    flow_a[k] = flow_a[k] - ta[k];
-    racc_b[k] = racc_b[k] + tb[k];
-    flow_b[k] = flow_b[k] - tb[k];
-  }
-  if (STORE && lane == 63) {  // column tau - 127 leaves stream b: its sum is final here
-    double* o = Fc + (size_t)(tau - 127) * D;
-#pragma unroll
-    for (int k = 0; k < D; ++k) agent_st(o + k, flow_b[k]);
-  }
-}
-
-template <int D, bool REPEL_ONE, bool DIAG_A, bool DIAG_B, bool STORE>
-__device__ __forceinline__ void pair_steps(bool fast, int t0, int t1, int lane, const double* rec,
-                                           const double* ini, double* Fc, const double (&xa)[D],
-                                           double da, const double (&xb)[D], double db,
-                                           double repel, double (&racc_a)[D], double (&flow_a)[D],
-                                           double (&racc_b)[D], double (&flow_b)[D]) {
-  if (fast) {
-    for (int tau = t0; tau < t1; ++tau)
-      pair_step<D, true, REPEL_ONE, DIAG_A, DIAG_B, STORE>(tau, lane, rec, ini, Fc, xa, da, xb,
-                                                           db, repel, racc_a, flow_a, racc_b,
-                                                           flow_b);
-  } else {
-    for (int tau = t0; tau < t1; ++tau)
-      pair_step<D, false, REPEL_ONE, DIAG_A, DIAG_B, STORE>(tau, lane, rec, ini, Fc, xa, da, xb,
-                                                            db, repel, racc_a, flow_a, racc_b,
-                                                            flow_b);
-  }
-}
-
-template <int D, bool REPEL_ONE, bool STAMP>
-__device__ __forceinline__ void pair_unit(int lane, int A, int base, int s, int* tprog,
-                                          const double* __restrict__ X,
-                                          const double* __restrict__ DP, double repel,
-                                          bool repel_ok, double* __restrict__ F, int* err,
-                                          long long limit, bool& give_up, double* rec,
-                                          double* ini, long long& spin, long long& t_first) {
-  constexpr int IW = SymI<D>::v;
-  const size_t cbase = (size_t)base + 64 * (size_t)A;
-  double* Fc = F + cbase * D;
-  const bool rva = 64 * A + lane < s, rvb = 64 * A + 64 + lane < s;
-  double xa[D], xb[D], racc_a[D], flow_a[D], racc_b[D], flow_b[D], da = 0.0, db = 0.0;
-#pragma unroll
-  for (int k = 0; k < D; ++k) {  // rows past the aggregate are inert
-    xa[k] = rva ? X[(cbase + lane) * D + k] : 0.0;
-    xb[k] = rvb ? X[(cbase + 64 + lane) * D + k] : 0.0;
-    racc_a[k] = flow_a[k] = racc_b[k] = flow_b[k] = 0.0;
-  }
-  if (rva) da = DP[cbase + lane];
-  if (rvb) db = DP[cbase + 64 + lane];
-  const bool rows_ok =
-      repel_ok && __all((!rva || vertex_ok<D>(xa, da)) && (!rvb || vertex_ok<D>(xb, db)));
-  const int ncols = s - 64 * A;
-  const int ntiles = (ncols + 63) >> 6;
-  const int tau_end = ncols + 127;  // the last column leaves stream b at step ncols + 126
-  bool ok1 = true, ok2 = true;      // column tiles tt-1 and tt-2 in the exact domain
-  for (int tt = 0; tt <= ntiles + 1; ++tt) {
-    const int qc = 64 * tt + lane;
-    const bool cv = qc < ncols;  // tiles past the aggregate stage inert records
-    if (A > 0 && tt < ntiles) {  // the units before have written column tile A + tt back
-      const long long w = handover_wait<STAMP>(tprog + tt, A, err, limit, give_up);
-      if (STAMP) {
-        spin += w;
-        if (tt == 0) t_first = rt_now();
-      }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // as in sweep_unit
-    }
-    double xc[D], ic[D], dc = 0.0;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
-      ic[k] = (cv && A > 0) ? agent_ld(F + (cbase + qc) * D + k) : 0.0;
-    }
-    if (cv) dc = DP[cbase + qc];
-    const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
-    double* rs = rec + (qc & (kPairRec - 1));
-    double* is = ini + (qc & (kPairIni - 1)) * IW;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      rs[k * kPairRec] = xc[k];
-      is[k] = ic[k];
-    }
-    rs[D * kPairRec] = dc;
-    wave_lds_sync();
-    const bool fast = rows_ok && ok_cur && ok1 && ok2;
-    const int t0 = 64 * tt, t1 = min(64 * tt + 64, tau_end);
-    if (tt < 2) {  // a's diagonal tile (b has not started: its lanes hold dead values)
-      pair_steps<D, REPEL_ONE, true, false, false>(fast, t0, t1, lane, rec, ini, Fc, xa, da, xb,
-                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
-    } else if (tt < 4) {  // b's diagonal tile; column 128 leaves b at the last step of tile 3
-      const int t1s = min(t1, 255);
-      pair_steps<D, REPEL_ONE, false, true, false>(fast, t0, t1s, lane, rec, ini, Fc, xa, da, xb,
-                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
-      pair_steps<D, REPEL_ONE, false, true, true>(fast, t1s, t1, lane, rec, ini, Fc, xa, da, xb,
-                                                  db, repel, racc_a, flow_a, racc_b, flow_b);
-    } else {
-      pair_steps<D, REPEL_ONE, false, false, true>(fast, t0, t1, lane, rec, ini, Fc, xa, da, xb,
-                                                   db, repel, racc_a, flow_a, racc_b, flow_b);
-    }
-    ok2 = ok1;
-    ok1 = ok_cur;
-    if (tt >= 4 && tt - 2 < ntiles) {
-      // column tile tt - 2 is in F: every store of it has completed (s_waitcnt 0)
-      // before the flag (see sym_handover)
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_waitcnt(0);
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (lane == 0)
-        __hip_atomic_store(tprog + tt - 2, A + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    wave_lds_sync();  // the slots staged next are free
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    if (rva) F[(cbase + lane) * D + k] = racc_a[k];
-    if (rvb) F[(cbase + 64 + lane) * D + k] = racc_b[k];
-  }
-}
-
-// One wave per block; units of kind 2 (pairs; the last of an aggregate with an odd
-// tile count has an inert stream b) and 1 (row blocks).
-// 4 waves per SIMD: <= 128 VGPRs
-template <int D, bool REPEL_ONE, bool STAMP = false>
-__global__ void __launch_bounds__(64, 4)
-faml_sym_pair(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
-              const int* __restrict__ pt_ip, const double* __restrict__ X,
-              const double* __restrict__ DP, double repel, double* __restrict__ F,
-              int* __restrict__ prog, int* __restrict__ err, long long limit,
-              long long* __restrict__ stamps) {
-  __shared__ __attribute__((aligned(16))) double arena[pair_arena_doubles<D>()];
-  const int lane = threadIdx.x;
-  const bool repel_ok = REPEL_ONE || weight_ok(repel);
-  bool give_up = false;
-  for (;;) {
-    int qi = 0;
-    if (lane == 0) qi = atomicAdd(queue, 1);
-    qi = __builtin_amdgcn_readfirstlane(qi);
-    if (qi >= nunits) break;  // every wave leaves once the queue is drained
-    long long t_take = 0, t_first = 0, spin = 0;
-    if (STAMP) t_take = t_first = rt_now();
-    const int4 u = units[qi];
-    const int A = u.y;
-    const int base = pt_ip[u.x];
-    const int s = pt_ip[u.x + 1] - base;
-    if (u.w == 1) {
-      __builtin_amdgcn_s_setprio(3);  // as in faml_sym_repulse
-      rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, arena, F);
-      __builtin_amdgcn_s_setprio(0);
-    } else {
-      pair_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel, repel_ok, F,
-                                     err, limit, give_up, arena, arena + (D + 1) * kPairRec, spin,
-                                     t_first);
     }
     if (STAMP && lane == 0) stamp_unit(stamps, qi, t_take, t_first, spin);
     wave_lds_sync();

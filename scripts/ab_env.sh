@@ -12,9 +12,10 @@ export TMPDIR=/tmp
 for r in $(seq 1 $ROUNDS); do
   for v in $VALS; do
     if [ "$v" = "-" ]; then unset $VAR; else export $VAR=$v; fi
-    f=$OUT/ab_${VAR}_${v}_$r.json
+    tagv=$(basename "$(dirname "$v")")_$(basename "$v")  # a path value names its directory
+    f=$OUT/ab_${VAR}_${tagv}_$r.json
     timeout -k 10 400 python -u bench.py --workload $W --steps 10 --warmup 2 --no-cpu-baseline \
-      --no-end-to-end > $f 2> $OUT/ab_${VAR}_${v}_$r.err || { tail -5 $OUT/ab_${VAR}_${v}_$r.err; exit 1; }
+      --no-end-to-end > $f 2> $OUT/ab_${VAR}_${tagv}_$r.err || { tail -5 $OUT/ab_${VAR}_${tagv}_$r.err; exit 1; }
     python3 -c "
 import json; d = json.load(open('$f'))
 print('$VAR=$v', round(d['ms_per_step'], 2), round(d['roofline']['avg_launch_ms'], 2),

@@ -11,7 +11,15 @@ The exchange goes through a local transport that copies the rank's own block int
 every slot (finite coordinates, host round trip), so the per-iteration wall time
 includes a PCIe copy RCCL would not make; the kernel times (repulse_ms, rows_ms)
 are unaffected, and the exchange is priced from its bytes at XGMI_GBS (bus
-bandwidth of an RCCL all-gather, default 300 GB/s)."""
+bandwidth of an RCCL all-gather, default 300 GB/s).
+
+WORKLOAD=c2 (configs[1]): the single-level forceAtlas on the
+1M-id R-MAT sharded by rows as bench.py --workload c2 --gpus N does it
+(ge_amd.dist.row_shards: contiguous vertex rows per rank, every rank's rows against
+all coordinates, one in-place all-gather of the coordinate array per iteration).
+Every rank's row-shard plan is timed on this GPU one after another (ITERS steps after
+one warm-up step); the all-gather of n * d * 8 bytes is priced at XGMI_GBS.  N = 1
+is the whole level (the symmetric sweeps); a shard runs the ordered-pair kernel."""
 import ctypes
 import json
 import os
@@ -45,7 +53,57 @@ def local_comm(ctx, N, r):
     return c
 
 
+def main_c2():
+    from ge_amd.dist import row_shards
+    dim, iters = 3, int(os.environ.get("ITERS", "2"))
+    ctx = ge.Context(0)
+    A = ctx.rmat_csr(1_000_000, 8_000_000, seed=12345)
+    n, nnz = len(A[0]) - 1, len(A[1])
+    dev = torch.device("cuda:0")
+    ip, ix, dx = (torch.from_numpy(a).to(dev) for a in A)
+    X0 = torch.from_numpy(ge.uniform_stream(12345, n * dim).reshape(n, dim)).to(dev)
+    gbs = float(os.environ.get("XGMI_GBS", "300"))
+    t1 = None
+    for N in [int(x) for x in os.environ.get("NS", "1,2,4,8").split(",")]:
+        chunk, shards = row_shards(n, N)
+        xa = torch.zeros((chunk * N, dim), dtype=torch.float64, device=dev)
+        xa[:n] = X0
+        xb = torch.zeros_like(xa)
+        times, reps, atts = [], [], []
+        for r in range(N):
+            rb, re = shards[r]
+            p = ctx.fa_plan(n, nnz, ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), dim, rb, re)
+            p.step(xa.data_ptr(), xb.data_ptr())  # warm-up (the symmetric plan's first launch)
+            ctx.sync()
+            p.set_profiling(True)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                p.step(xa.data_ptr(), xb.data_ptr())
+            ctx.sync()
+            times.append((time.perf_counter() - t0) / iters * 1e3)
+            rep_ms, att_ms, _ = p.kernel_ms()
+            reps.append(rep_ms)
+            atts.append(att_ms)
+            p.close()
+            print(f"N={N} rank {r}: rows [{rb}, {re}) {times[-1]:.1f} ms per step", file=sys.stderr,
+                  flush=True)
+        xbytes = n * dim * 8
+        ag_ms = xbytes * (N - 1) / N / (gbs * 1e9) * 1e3 if N > 1 else 0.0
+        step = max(times) + ag_ms
+        t1 = t1 or step
+        print(json.dumps({"workload": "c2", "N": N, "ms_per_step_by_rank": times,
+                          "repulse_ms_by_rank": reps, "attract_ms_by_rank": atts,
+                          "allgather_bytes": xbytes if N > 1 else 0,
+                          "allgather_ms_priced": ag_ms, "max_ms": step,
+                          "efficiency": t1 / (N * step),
+                          "kernel": "symmetric sweeps" if N == 1 else "ordered-pair row shards"}),
+              flush=True)
+    ctx.close()
+
+
 def main():
+    if os.environ.get("WORKLOAD") == "c2":
+        return main_c2()
     n, draws, dim, iters = 10_000_000, 80_000_000, 3, int(os.environ.get("ITERS", "5"))
     ctx = ge.Context(0)
     L = ctx.rmat_csr(n, draws, seed=12345, lcc=True)

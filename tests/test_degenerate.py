@@ -150,34 +150,3 @@ def test_fa_flat_dimension_signed_zeros(ctx, oracle):
     want = oracle.force_atlas(A, 3, coords=X0, iterations=5)
     got = ctx.force_atlas(A, 3, coords=X0, iterations=5)
     assert np.array_equal(got, want)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("copy", ["1", "0"])
-@pytest.mark.parametrize("rows", [(0, 3000), (700, 2100)])
-def test_fa_gather_copy(ctx, oracle, monkeypatch, copy, rows):
-    """Attraction gathers from the degree-ordered copy of the coordinates
-    (GE_GATHER_COPY=1, remapped CSR indices) or from X itself: same bits, also for
-    a row shard (remapped indices offset by the shard's first entry) and with
-    hub rows split into segments."""
-    monkeypatch.setenv("GE_STREAM_MAX", "0")
-    monkeypatch.setenv("GE_GATHER_COPY", copy)
-    n = 3000
-    A = G.with_hubs(G.rmat(n, 8 * n, seed=21), [(5, 1500), (2000, 900)], seed=2)
-    X0 = G.random_coords(n, 3, seed=8)
-    want = oracle.force_atlas(A, 3, coords=X0, iterations=4)
-    if rows == (0, n):
-        assert np.array_equal(ctx.force_atlas(A, 3, coords=X0, iterations=4), want)
-    else:
-        import torch
-        one = oracle.force_atlas(A, 3, coords=X0, iterations=1)
-        dev = torch.device("cuda:0")
-        ip, ix, dx = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in A)
-        x = torch.from_numpy(X0).to(dev)
-        y = torch.zeros_like(x)
-        plan = ctx.fa_plan(n, len(A[1]), ip.data_ptr(), ix.data_ptr(), dx.data_ptr(), 3, *rows)
-        plan.step(x.data_ptr(), y.data_ptr())
-        ctx.sync()
-        got = y.cpu().numpy()
-        plan.close()
-        assert np.array_equal(got[rows[0]:rows[1]], one[rows[0]:rows[1]])

@@ -135,11 +135,8 @@ def test_c4_level0_schedules_agree_at_embed_horizon(ctx, monkeypatch, heartbeat)
     rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
     runs = {}
     for name, env in (("sweeps", {}), ("row_blocks", {"GE_FAML_SYM_CHAIN": "1e9"}),
-                      ("row_blocks_tail_split", {"GE_FAML_SYM_CHAIN": "1e9",
-                                                 "GE_FAML_TAILSPLIT_K": "20000",
-                                                 "GE_FAML_TAILSPLIT_F": "0.7"}),
                       ("ordered_pairs", {"GE_FAML_SYM": "0"})):
-        for k in ("GE_FAML_SYM_CHAIN", "GE_FAML_SYM", "GE_FAML_TAILSPLIT_K", "GE_FAML_TAILSPLIT_F"):
+        for k in ("GE_FAML_SYM_CHAIN", "GE_FAML_SYM"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -148,7 +145,6 @@ def test_c4_level0_schedules_agree_at_embed_horizon(ctx, monkeypatch, heartbeat)
         _progress(t0, f"C4 {name} done")
     assert np.isfinite(runs["sweeps"]).all()
     assert np.array_equal(runs["sweeps"], runs["row_blocks"])
-    assert np.array_equal(runs["sweeps"], runs["row_blocks_tail_split"])
     assert np.array_equal(runs["sweeps"], runs["ordered_pairs"])
 
 

@@ -533,29 +533,6 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, re
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("sym,dim", [("1", 3), ("0", 3), ("1", 2), ("1", 4)])
-def test_faml_rows_early_segments(ctx, oracle, monkeypatch, sym, dim):
-    """GE_ROWS_EARLY=1 (ge_rows.hpp launch_rows_early): the heavy member rows'
-    segment terms queued beside the streamed repulsion launch, their chains and the
-    tiles after it -- symmetric sweeps and the ordered-pair kernel, hub rows longer
-    than one segment."""
-    monkeypatch.setenv("GE_ROWS_EARLY", "1")
-    monkeypatch.setenv("GE_ROWS_TILES", "1")
-    monkeypatch.setenv("GE_FAML_SYM", sym)
-    sizes = [3000, 700, 2203, 90, 1]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=9), [(3, 2600), (40, 5000)], seed=dim)
-    assert np.diff(A[0]).max() > 4096
-    PT = _block_partition(n, sizes, seed=4)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=19)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=19)
-    assert np.array_equal(got, want)
-
-
 @pytest.mark.parametrize("chain,dim,repel", [
     ("0", 3, 1.0), ("0", 3, 1.5), ("0", 3, 2.0 ** 70), ("1e9", 3, 1.0), ("", 3, 1.0),
     ("0", 2, 1.0), ("0", 4, 0.75), ("1e9", 4, 1.0)])
@@ -578,103 +555,6 @@ def test_faml_symmetric_sweeps(ctx, oracle, monkeypatch, chain, dim, repel):
     rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
     want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
     got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=6, seed=19, repel=repel)
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("seg,dim,repel", [("4", 3, 1.0), ("7", 3, 2.0 ** 70), ("3", 2, 1.5),
-                                           ("5", 4, 1.0), ("1", 3, 1.0)])
-def test_faml_segmented_row_blocks(ctx, oracle, monkeypatch, seg, dim, repel):
-    """Row blocks cut into column segments of `seg` tiles (ge_sym.hpp kind 5): each
-    segment continues its rows' sums from the one before through F, layer after
-    layer in the queue; ragged last segments, one-tile segments, the `/` path."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "1e9")  # every streamed aggregate as row blocks
-    monkeypatch.setenv("GE_FAML_ROWSEG", seg)
-    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=17), [(3, 2000), (70, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=7)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m + 2)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=29, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=29, repel=repel)
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("k,f,dim,repel", [("100000", "0.5", 3, 1.0), ("100000", "0.9", 3, 2.0 ** 70),
-                                           ("7", "0.1", 3, 1.5), ("100000", "0.6", 2, 1.0),
-                                           ("3", "0.7", 4, 1.0)])
-def test_faml_tail_split_row_blocks(ctx, oracle, monkeypatch, k, f, dim, repel):
-    """Tail split (ge_faml.hip faml_plan_build): the k smallest row blocks of an
-    all-row-block plan cut into a head segment (columns [0, 64 round(f T))) at the
-    front of the queue and a tail segment continuing the rows' sums at its end;
-    every block cut or a few, heads of one tile (f = 0.1 on small aggregates), the
-    `/` path, every dimension."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "1e9")  # every streamed aggregate as row blocks
-    monkeypatch.setenv("GE_FAML_TAILSPLIT_K", k)
-    monkeypatch.setenv("GE_FAML_TAILSPLIT_F", f)
-    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=19), [(3, 2000), (70, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=8)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m + 3)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=31, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=31, repel=repel)
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("bands,dim,repel", [
-    ("2", 3, 1.0), ("3", 3, 1.0), ("4", 3, 1.5), ("8", 3, 1.0), ("2", 3, 2.0 ** 70),
-    ("3", 2, 1.0), ("4", 4, 0.75), ("2", 1, 1.0)])
-def test_faml_symmetric_bands(ctx, oracle, monkeypatch, bands, dim, repel):
-    """Banded aggregates (ge_sym.hpp): each streamed aggregate cut into K bands of
-    row tiles -- pre row blocks (the band's rows against the members before it,
-    handed to the band's first sweep as entering column sums), in-band sweeps, post
-    row blocks continuing from the sweeps' row sums -- keep every row's order of
-    additions; K = 2..8 (capped at half the tiles), the `/` path, every dimension."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_SYM_BANDS", bands)
-    sizes = [2600, 320, 700, 257, 1031, 300, 90, 1]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=13), [(3, 2000), (70, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=6)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m + 1)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=23, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=4, seed=23, repel=repel)
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("pair,dim,repel", [
-    ("1", 3, 1.0), ("1", 3, 2.0 ** 70), ("1", 2, 1.5), ("1", 4, 1.0), ("0", 3, 1.0),
-    ("0", 3, 2.0 ** 70)])
-def test_faml_symmetric_pairs(ctx, oracle, monkeypatch, pair, dim, repel):
-    """faml_sym_pair (ge_sym.hpp): two row tiles per wave (stream b 128 steps
-    behind stream a), the hand-over every second row tile; even and odd tile
-    counts (the odd one ends with a single sweep), ragged last tiles, one-member
-    last tiles, last pairs of two tiles (no hand-over), hub rows; against the oracle
-    and against the one-tile-per-wave kernel (pair = 0)."""
-    monkeypatch.setenv("GE_FAML_SYM", "1")
-    monkeypatch.setenv("GE_FAML_SYM_CHAIN", "0")
-    monkeypatch.setenv("GE_FAML_SYM_PAIR", pair)
-    sizes = [2560, 383, 704, 257, 1089, 300, 448, 90, 1, 4100]
-    n = sum(sizes)
-    A = G.with_hubs(G.rmat(n, 10 * n, seed=13), [(5, 2500), (2600, 3000)], seed=dim)
-    PT = _block_partition(n, sizes, seed=7)
-    vA = ge.vertex_of(PT)
-    m = len(sizes)
-    cA = G.random_coords(m, dim, seed=m + 1)
-    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
-    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=23, repel=repel)
-    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=5, seed=23, repel=repel)
     assert np.array_equal(got, want)
 
 
