@@ -64,29 +64,47 @@ __device__ __forceinline__ void agent_st(double* p, double v) {
 
 __device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
-constexpr int kSymRing = 128;  // LDS ring of column slots (column q at q & 127)
+// LDS of one sweep wave (round 5).  Column q of the sweep (q = column - 64 A) keeps
+// its running sum in LDS, in slot q & 127 of the column ring `col` (D components, 128
+// slots each): at step s lane l reads the sum of column s - l, subtracts its term and
+// writes it back, and one step later lane l + 1 reads what lane l wrote -- one wave's
+// DS instructions execute in issue order, and a compiler barrier between the steps
+// keeps their order in the code.  Before round 5 the sums travelled in registers one
+// lane per step (a DPP wave shift: 6 moves per step at D = 3) with a broadcast read
+// of the entering sum and a predicated store of the leaving one; here none of them.
+// The column's entering sum (from the sweeps before) is staged into its slot, and
+// its final sum is in the slot once lane 63 has passed it.
+// Records {x[D], deg+1} are component-major in the ring `rec` (D + 1 components,
+// kRecSlots slots each): column q at slot q & 127, and slots 0..63 mirrored at
+// 128..191, so that within a column tile every lane reads slot ((64 tt - l) & 127) + j
+// at step 64 tt + j without wrapping: the per-step addresses are immediate offsets.
+// The column ring wraps inside the even tiles only (tile tt holds slots
+// 64 (tt & 1) .. +63): there a lane switches base once.
+constexpr int kSymRing = 128;   // column ring (column q at q & 127)
+constexpr int kRecSlots = 192;  // record ring: 128 slots + the first 64 mirrored
 
-template <int D>
-struct SymI {
-  static constexpr int v = D;  // column-sum slot width (3 KB per 128-slot ring at D = 3)
-};
+// Compiler barrier between two steps: the next step's reads of the column ring
+// must stay after this step's writes (different slots for one lane, the same slot
+// for the next lane: a cross-lane dependency the compiler cannot see).
+__device__ __forceinline__ void step_barrier() { asm volatile("" ::: "memory"); }
 
-// Steps [s0, s1) of a sweep.  DIAG: the steps may meet the diagonal tile
-// (s < 127), where a lane takes the travelling sum of its own row over.  The LDS
-// reads of step s + 1 (entering column sum, partner record) are issued before
-// step s computes: both were staged before the steps began.
+// One step of a sweep at any position (runtime step index sg): the diagonal tiles
+// (DIAG: a lane takes its own row's sum over from the column that reaches it), the
+// drain, and tiles outside the shared-reciprocal domain (SHARED = false).
 template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void sym_step(int sg, int lane, int ncols, double* out,
-                                         const double (&xr)[D], double dr, bool rv, double repel,
-                                         const double (&in0)[D], const double (&xq)[D + 1],
-                                         double (&racc)[D], double (&flow)[D]) {
-  constexpr int IW = SymI<D>::v;
-  // column sg enters lane 0 with its stored sum
+__device__ __forceinline__ void col_step(int sg, int lane, const double* rec, double* col,
+                                         const double (&xr)[D], double dr, double repel,
+                                         double (&racc)[D]) {
+  const int q = sg - lane;
+  const int p = q & (kSymRing - 1);
+  double xq[D + 1], c[D];
 #pragma unroll
-  for (int k = 0; k < D; ++k) flow[k] = wave_shift_in(flow[k], in0[k]);
-  if (DIAG && sg - lane == lane) {
+  for (int k = 0; k <= D; ++k) xq[k] = rec[k * kRecSlots + p];
 #pragma unroll
-    for (int k = 0; k < D; ++k) racc[k] = flow[k];
+  for (int k = 0; k < D; ++k) c[k] = col[k * kSymRing + p];
+  if (DIAG && q == lane) {  // column q = this lane's row: its sum so far is the row's
+#pragma unroll
+    for (int k = 0; k < D; ++k) racc[k] = c[k];
   }
   // Every lane evaluates a term every step (no divergent exec mask): a pair with
   // an inert row or column (deg+1 = 0) and the self pair are +-0, which leave a
@@ -94,60 +112,74 @@ __device__ __forceinline__ void sym_step(int sg, int lane, int ncols, double* ou
   // and the absorbed columns' sums are dead values.
   double t[D];
   rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
-  if (!SHARED && DIAG && sg - lane == lane) {  // the `/` form skips the self pair (ge_pair.hpp)
+  if (!SHARED && DIAG && q == lane) {  // the `/` form skips the self pair (ge_pair.hpp)
 #pragma unroll
     for (int k = 0; k < D; ++k) t[k] = 0.0;
   }
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     racc[k] = racc[k] + t[k];
-    flow[k] = flow[k] - t[k];
+    col[k * kSymRing + p] = c[k] - t[k];
   }
-  if (lane == 63) {  // column sg - 63 leaves the wave
-    double* o = out + ((sg - 63) & (kSymRing - 1)) * IW;
+  step_barrier();
+}
+
+template <int D, bool REPEL_ONE, bool DIAG>
+__device__ __forceinline__ void col_steps(bool fast, int s0, int s1, int lane, const double* rec,
+                                          double* col, const double (&xr)[D], double dr,
+                                          double repel, double (&racc)[D]) {
+  if (fast)
+    for (int sg = s0; sg < s1; ++sg)
+      col_step<D, true, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc);
+  else
+    for (int sg = s0; sg < s1; ++sg)
+      col_step<D, false, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc);
+}
+
+// The 64 steps of a full column tile tt >= 2 in the shared-reciprocal domain (the
+// bulk of every sweep): eight blocks of eight steps, every LDS access an immediate
+// offset from a per-block base.  EVEN: tt even, where lanes l > j read slot
+// 128 + j - l and lanes l <= j slot j - l (one select per step).  No prefetch of the
+// next step's records into a second register set: the other waves of the SIMD hide
+// the LDS latency, and the kernel must stay within 120 VGPRs (see faml_sym_repulse).
+template <int D, bool REPEL_ONE, bool EVEN>
+__device__ __forceinline__ void tile_steps(int tt, int lane, const double* rec, double* col,
+                                           const double (&xr)[D], double dr, double repel,
+                                           double (&racc)[D]) {
+  const double* rb = rec + ((64 * tt - lane) & (kSymRing - 1));
+  double* cb = col + (EVEN ? kSymRing - lane : 64 - lane);
+  for (int j0 = 0; j0 < 64; j0 += 8) {
+    const double* rj = rb + j0;
+    double* cj = cb + j0;
 #pragma unroll
-    for (int k = 0; k < D; ++k) o[k] = flow[k];
+    for (int jj = 0; jj < 8; ++jj) {
+      double* cp = cj + jj;
+      if (EVEN && j0 + jj >= lane) cp -= kSymRing;
+      double c[D], xq[D + 1];
+#pragma unroll
+      for (int k = 0; k <= D; ++k) xq[k] = rj[k * kRecSlots + jj];
+#pragma unroll
+      for (int k = 0; k < D; ++k) c[k] = cp[k * kSymRing];
+      double t[D];
+      rep_term<D, true, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        racc[k] = racc[k] + t[k];
+        cp[k * kSymRing] = c[k] - t[k];
+      }
+      step_barrier();
+    }
   }
 }
 
-// LDS reads of one step: the entering column sum (broadcast) and the partner record
-template <int D>
-__device__ __forceinline__ void sym_fetch(int sg, int lane, const double* rec, const double* ini,
-                                          double (&i0)[D], double (&xv)[D + 1]) {
-  constexpr int WV = SymW<D>::v;
-  constexpr int IW = SymI<D>::v;
-  const double* ic = ini + (sg & (kSymRing - 1)) * IW;
-  // records are stored by component (rec[k][slot]): consecutive lanes read
-  // consecutive slots, no bank conflicts
-  const int slot = (sg - lane) & (kSymRing - 1);
-#pragma unroll
-  for (int k = 0; k < D; ++k) i0[k] = ic[k];
-#pragma unroll
-  for (int k = 0; k <= D; ++k) xv[k] = rec[k * kSymRing + slot];
-}
-
-// Steps [s0, s1) of a sweep.  DIAG: the steps may meet the diagonal tile
-// (s < 127), where a lane takes the travelling sum of its own row over.  The LDS
-// reads of step s + 1 are issued before step s computes (both slots were staged
-// before the steps began); two register sets alternate.
-template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void sym_steps(int s0, int s1, int lane, int ncols, const double* rec,
-                                          const double* ini, double* out,
-                                          const double (&xr)[D], double dr, bool rv, double repel,
-                                          double (&racc)[D], double (&flow)[D]) {
-  if (s0 >= s1) return;
-  double ia[D], xa[D + 1], ib[D], xb[D + 1];
-  sym_fetch<D>(s0, lane, rec, ini, ia, xa);
-  for (int sg = s0;; sg += 2) {
-    sym_fetch<D>(sg + 1, lane, rec, ini, ib, xb);
-    sym_step<D, SHARED, REPEL_ONE, DIAG>(sg, lane, ncols, out, xr, dr, rv, repel, ia, xa, racc,
-                                         flow);
-    if (sg + 1 >= s1) break;
-    sym_fetch<D>(sg + 2, lane, rec, ini, ia, xa);
-    sym_step<D, SHARED, REPEL_ONE, DIAG>(sg + 1, lane, ncols, out, xr, dr, rv, repel, ib, xb,
-                                         racc, flow);
-    if (sg + 2 >= s1) break;
-  }
+template <int D, bool REPEL_ONE>
+__device__ __forceinline__ void tile_steps_any(int tt, int lane, const double* rec, double* col,
+                                               const double (&xr)[D], double dr, double repel,
+                                               double (&racc)[D]) {
+  if (tt & 1)
+    tile_steps<D, REPEL_ONE, false>(tt, lane, rec, col, xr, dr, repel, racc);
+  else
+    tile_steps<D, REPEL_ONE, true>(tt, lane, rec, col, xr, dr, repel, racc);
 }
 
 // Hand-over slot of member c, dimension k: component-major H[k * hs + c].
@@ -163,15 +195,14 @@ __device__ __forceinline__ double* hand_at(double* H, size_t hs, size_t c, int k
 // 24-byte-strided record store spans, which the agent-scope stores pay per line.
 template <int D>
 __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncols, size_t cbase,
-                                             const double* out, double* H, size_t hs,
+                                             const double* col, double* H, size_t hs,
                                              int* tprog) {
-  constexpr int IW = SymI<D>::v;
   wave_lds_sync();
   const int qo = 64 * t + lane;
   if (qo < ncols) {
-    const double* o = out + (qo & (kSymRing - 1)) * IW;
+    const double* o = col + (qo & (kSymRing - 1));
 #pragma unroll
-    for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, cbase + qo, k), o[k]);
+    for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, cbase + qo, k), o[k * kSymRing]);
   }
   // Ordering (no acquire/release: an agent-scope release would write back the whole
   // L2, ~every 64 steps): the sums are agent-scope stores (they bypass the per-XCD
@@ -223,19 +254,6 @@ __device__ __forceinline__ long long handover_wait(const int* flag, int A, int* 
     }
   }
   return STAMP ? rt_now() - t0 : 0;
-}
-
-template <int D, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void sym_steps_any(bool fast, int s0, int s1, int lane, int ncols,
-                                              const double* rec, const double* ini, double* out,
-                                              const double (&xr)[D], double dr, bool rv,
-                                              double repel, double (&racc)[D], double (&flow)[D]) {
-  if (fast)
-    sym_steps<D, true, REPEL_ONE, DIAG>(s0, s1, lane, ncols, rec, ini, out, xr, dr, rv, repel,
-                                        racc, flow);
-  else
-    sym_steps<D, false, REPEL_ONE, DIAG>(s0, s1, lane, ncols, rec, ini, out, xr, dr, rv, repel,
-                                         racc, flow);
 }
 
 // A row block: the 64 rows of tile A against the members [c0, c1) in ascending
@@ -317,8 +335,8 @@ constexpr int kStampWords = 8;
 
 
 // One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
-// column sums handed to the next sweep tile by tile.  rec / ini / out: this wave's
-// rings (kSymRing slots each).  STAMP: spin ticks and the first hand-over time.
+// column sums handed to the next sweep tile by tile.  rec / col: this wave's rings
+// (see kSymRing).  STAMP: spin ticks and the first hand-over time.
 template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false>
 __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
                                            const double* __restrict__ X,
@@ -326,17 +344,15 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
                                            bool repel_ok, double* __restrict__ F,
                                            double* __restrict__ H, size_t hs, int* err,
                                            long long limit, bool& give_up, double* rec,
-                                           double* ini, double* out, long long& spin,
-                                           long long& t_first, double (&rout)[D]) {
-  constexpr int IW = SymI<D>::v;
+                                           double* col, long long& spin, long long& t_first,
+                                           double (&rout)[D]) {
   const size_t cbase = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
-  double xr[D], racc[D], flow[D], dr = 0.0;  // a row past the aggregate is inert
+  double xr[D], racc[D], dr = 0.0;  // a row past the aggregate is inert
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
     racc[k] = 0.0;
-    flow[k] = 0.0;
   }
   if (rv) dr = DP[cbase + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
@@ -365,44 +381,49 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     }
     if (cv) dc = DP[cbase + qc];
     const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
-    double* rs = rec + (qc & (kSymRing - 1));
-    double* is = ini + (qc & (kSymRing - 1)) * IW;
+    const int p = qc & (kSymRing - 1);
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      rs[k * kSymRing] = xc[k];
-      is[k] = ic[k];
+      rec[k * kRecSlots + p] = xc[k];
+      col[k * kSymRing + p] = ic[k];  // the column enters with its sum so far
     }
-    rs[D * kSymRing] = dc;
+    rec[D * kRecSlots + p] = dc;
+    if (!(tt & 1)) {  // slots 0..63 are mirrored at 128..191
+#pragma unroll
+      for (int k = 0; k < D; ++k) rec[k * kRecSlots + p + kSymRing] = xc[k];
+      rec[D * kRecSlots + p + kSymRing] = dc;
+    }
     wave_lds_sync();
     // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
     const bool fast = rows_ok && ok_cur && ok_prev;
     if (tt < 2)
-      sym_steps_any<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini, out,
-                                        xr, dr, rv, repel, racc, flow);
+      col_steps<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
+                                    racc);
+    else if (fast)
+      tile_steps_any<D, REPEL_ONE>(tt, lane, rec, col, xr, dr, repel, racc);
     else
-      sym_steps_any<D, REPEL_ONE, false>(fast, 64 * tt, 64 * tt + 64, lane, ncols, rec, ini,
-                                         out, xr, dr, rv, repel, racc, flow);
+      col_steps<D, REPEL_ONE, false>(false, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
+                                     racc);
     ok_prev = ok_cur;
-    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
+    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, col, H, hs, tprog);
     wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
   }
   {  // drain: the last columns cross the wave; the slots past them hold inert records
-    double* rs = rec + ((64 * ntiles + lane) & (kSymRing - 1));
-    double* is = ini + ((64 * ntiles + lane) & (kSymRing - 1)) * IW;
+    const int p = (64 * ntiles + lane) & (kSymRing - 1);
 #pragma unroll
-    for (int k = 0; k <= D; ++k) rs[k * kSymRing] = 0.0;
-#pragma unroll
-    for (int k = 0; k < D; ++k) is[k] = 0.0;
+    for (int k = 0; k <= D; ++k) {
+      rec[k * kRecSlots + p] = 0.0;
+      if (!(ntiles & 1)) rec[k * kRecSlots + p + kSymRing] = 0.0;
+    }
     wave_lds_sync();
   }
   const int s0 = 64 * ntiles, s1 = ncols + 63;
   if (ntiles < 2)
-    sym_steps_any<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
-                                      xr, dr, rv, repel, racc, flow);
+    col_steps<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel, racc);
   else
-    sym_steps_any<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, ncols, rec, ini, out,
-                                       xr, dr, rv, repel, racc, flow);
-  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, out, H, hs, tprog);
+    col_steps<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel,
+                                   racc);
+  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, col, H, hs, tprog);
   // the rows' sums: the caller writes them to F
 #pragma unroll
   for (int k = 0; k < D; ++k) rout[k] = racc[k];
@@ -446,16 +467,15 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
                  double* __restrict__ H, size_t hs, int* __restrict__ prog,
                  int* __restrict__ err, long long limit, long long* __restrict__ stamps) {
-  constexpr int WV = SymW<D>::v;
-  constexpr int IW = SymI<D>::v;
   constexpr int NW = kSymT / 64;
-  __shared__ __attribute__((aligned(16))) double srec[NW][kSymRing * WV];
-  __shared__ __attribute__((aligned(16))) double sini[NW][kSymRing * IW];
-  __shared__ __attribute__((aligned(16))) double sout[NW][kSymRing * IW];
+  // per wave: the record ring (also the row blocks' tile: 64 records of SymW<D>
+  // doubles) and the column ring
+  static_assert(kRecSlots * (D + 1) >= 64 * SymW<D>::v, "row-block tile fits the record ring");
+  __shared__ __attribute__((aligned(16))) double srec[NW][kRecSlots * (D + 1)];
+  __shared__ __attribute__((aligned(16))) double scol[NW][kSymRing * D];
   const int lane = threadIdx.x & 63;
   double* rec = srec[threadIdx.x >> 6];
-  double* ini = sini[threadIdx.x >> 6];
-  double* out = sout[threadIdx.x >> 6];
+  double* col = scol[threadIdx.x >> 6];
   const bool repel_ok = REPEL_ONE || weight_ok(repel);
   bool give_up = false;  // a hand-over wait timed out (err is set on exit)
   for (;;) {
@@ -479,8 +499,8 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     } else {  // a sweep
       double racc[D];
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
-                                              repel_ok, F, H, hs, err, limit, give_up, rec, ini,
-                                              out, spin, t_first, racc);
+                                              repel_ok, F, H, hs, err, limit, give_up, rec, col,
+                                              spin, t_first, racc);
       if (64 * A + lane < s) {
 #pragma unroll
         for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = racc[k];
