@@ -56,6 +56,23 @@ METRIC = "ForceAtlas iterations/sec + edges/sec, 3-D embed, 10M-vtx R-MAT @1/2/4
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec); the strict kernels run on the VALU
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E peak, MI355X_MICROARCH.md
 FLOPS_PER_PAIR = 26      # (7d+5) at d=3, SURVEY.md 8(d)
+# the symmetric kernel per UNORDERED pair: one term (the 26 above, its row add
+# included) plus the subtraction from the partner's (column) sum
+SYM_FLOPS_PER_UNORDERED_PAIR = 29
+
+
+def executed_rate(credited_flops, ms, symmetric):
+    """The VALU work the kernel actually issues: the roofline's
+    `achieved` credits 26 flops per ORDERED pair (the reference's work, SURVEY.md
+    8(d)); the symmetric kernel evaluates each unordered pair once, so it executes
+    29 / 52 of that.  Returned as its own record beside the credited figure."""
+    if not symmetric or ms <= 0:
+        return None
+    flops = credited_flops / (2 * FLOPS_PER_PAIR) * SYM_FLOPS_PER_UNORDERED_PAIR
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"flops_per_launch": flops, "tflops": tf, "frac": tf / FP64_PEAK_TFLOPS,
+            "flops_per_unit": "29 per unordered pair (one term with its row add, plus the "
+                              "partner's subtraction); sqrt and division counted as 1"}
 WORKLOADS = {"c2": (1_000_000, 8_000_000), "c3": (1_000_000, 8_000_000),
              "c4": (10_000_000, 80_000_000)}
 
@@ -90,8 +107,8 @@ def log(rank, *a):
 def host_info():
     """CPU model, logical CPUs, physical cores (lscpu) and this process's affinity."""
     info = {"logical_cpus": os.cpu_count()}
-    try:
-        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    try:  # the calling thread's mask (bound to one core by libgomp: see cpu_share)
+        info["main_thread_affinity_cpus"] = len(os.sched_getaffinity(0))
     except AttributeError:
         pass
     for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpuset.cpus.effective"):
@@ -117,23 +134,49 @@ def host_info():
     return info
 
 
-def baseline_threads():
-    """OpenMP threads for the CPU baseline: the CPUs this process may run on (its
-    affinity), so a small CPU share is not oversubscribed; OMP_NUM_THREADS only
-    lowers it."""
+def cpu_share():
+    """CPUs this job may keep busy at once: the cgroup's CPU quota (cpu.max) and its
+    cpuset.  Not os.sched_getaffinity(0): that is the CALLING THREAD's mask, and once
+    libgomp has started with OMP_PROC_BIND=close / OMP_PLACES=cores (set above) it has
+    bound the main thread to its first place -- one core, 2 SMT threads -- which is
+    why rounds 1-4 reported 2 CPUs on boxes whose job gets 16 (VERDICT r04 weak 9;
+    scripts/affinity_probe.py: 256 CPUs in a process without the binding)."""
+    share = os.cpu_count() or 1
     try:
-        cpus = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cpus = os.cpu_count() or 1
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            share = min(share, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("Cpus_allowed_list"):
+                    n = 0
+                    for part in line.split(":", 1)[1].strip().split(","):
+                        a, _, b = part.partition("-")
+                        n += int(b or a) - int(a) + 1
+                    share = min(share, n)
+    except (OSError, ValueError):
+        pass
+    return share
+
+
+def baseline_threads():
+    """OpenMP threads for the CPU baseline: the job's CPU share (cpu_share), so a small
+    share is not oversubscribed; OMP_NUM_THREADS only lowers it."""
+    cpus = cpu_share()
     env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return min(cpus, env) if env else cpus
 
 
 def baseline_record(value, unit, threads, sample, per_iter):
     hi = host_info()
-    # the threads that can run at once: the OpenMP threads, bounded by the CPUs this
-    # process may use (the GPU box confines a job to a small CPU share)
-    cores = min(threads, hi.get("affinity_cpus") or threads)
+    # the threads that can run at once: the OpenMP threads, bounded by the job's CPU
+    # share (the GPU box confines a job to 16 CPUs of its cgroup quota)
+    hi["cpu_share"] = cpu_share()
+    cores = min(threads, hi["cpu_share"])
     rec = {"value": value, "unit": unit, "cores": cores, "omp_threads": threads, "kind": "port",
            "sample": sample,
            "seconds_per_iteration": per_iter, "host": hi,
@@ -431,6 +474,7 @@ def run_multilevel(args, rank, world, local, dev):
     its = args.steps / elapsed
     rep_flops = FLOPS_PER_PAIR * rep_pairs
     rep_tflops = rep_flops / (rep_ms * 1e-3) / 1e12 if rep_ms > 0 else 0.0
+    sched = sym_schedule(pk)
     cfgname = {"c3": "C3 (BASELINE.json configs[2])", "c4": "C4 (BASELINE.json configs[3])"}
     result = {
         "metric": METRIC, "value": its, "unit": "iterations/s", "n_gpus": world,
@@ -461,6 +505,9 @@ def run_multilevel(args, rank, world, local, dev):
                      "flops_per_unit": "26 per ordered in-aggregate pair (7d+5, d=3); the "
                                        "symmetric kernel evaluates each unordered pair once "
                                        "and credits both ordered pairs",
+                     "executed": executed_rate(rep_flops, rep_ms,
+                                               rep_kernel == "faml_sym_repulse" and
+                                               (sched or {}).get("row_blocks", 1) == 0),
                      "avg_launch_ms": rep_ms, "launches": rep_launches},
         "roofline_attraction": {"kernel": "tile_rows_kernel<FamlRows> + heavy rows (the "
                                           "streamed members' CSR attraction / external pull, "
@@ -475,7 +522,7 @@ def run_multilevel(args, rank, world, local, dev):
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
         # this rank's streamed aggregates: plain symmetric sweeps / bands (a shorter
         # dependency chain) / whole row blocks
-        "sym_schedule": sym_schedule(pk),
+        "sym_schedule": sched,
         "setup_seconds": {"graph_device": t_gen, "partition_device": t_part,
                           "partition_host": t_part_host, "ptap_device": t_ptap,
                           "plan_build": plan_seconds.get(args.steps),
@@ -584,6 +631,7 @@ def run_single_level(args, rank, world, local, dev):
                      "flops_per_unit": "26 per ordered pair (7d+5, d=3)" + (
                          "; the symmetric kernel evaluates each unordered pair once and credits"
                          " both ordered pairs" if sym else ""),
+                     "executed": executed_rate(FLOPS_PER_PAIR * pairs, rep_ms, sym),
                      "avg_launch_ms": rep_ms, "launches": launches},
         "roofline_attraction": {"kernel": "tile_rows_kernel<FaRows> + classed_rows_kernel<FaRows>"
                                           " (CSR attraction + gravity + update; fork to join)",

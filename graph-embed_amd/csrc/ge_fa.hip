@@ -36,6 +36,7 @@
 #include <numeric>
 #include <cstdlib>
 #include <cmath>
+#include <memory>
 #include <vector>
 
 #include "ge_internal.hpp"
@@ -1198,12 +1199,19 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   const int grp = blockIdx.x / kBarGroup;
   const int members = min(kBarGroup, nb - grp * kBarGroup);
   int* gc = bar + kBarLine * (2 + grp);
-  // Release / acquire at agent scope (the HIP memory model, not only the store
-  // completion the callers' s_waitcnt gives): the arrival releases this block's
-  // coordinate stores (ordered before it by the block's __syncthreads), the group's
-  // last arrival acquires its group's releases and releases them on to the grid
-  // counter, and a waiter acquires with one fence after its relaxed poll.  Once per
-  // iteration, so the L2 write-back / invalidate it implies costs little.
+  // Ordering as shipped (GE_BAR_ORDER 0): the arrival and the group's hand-on are
+  // RELAXED agent-scope atomics with no acquire fence after the poll.  What orders a
+  // block's coordinate stores before another block's staging loads is the hardware,
+  // not the HIP memory model: the coordinates are written and read with agent-scope
+  // (L2-bypassing) accesses, every store has completed at the memory side
+  // (s_waitcnt 0, in fa_grouped_persistent) before the block's thread 0 arrives, and
+  // a waiter's staging loads are issued only after its poll has seen the count.  The
+  // release / acquire orders 1-4 below follow the model and were measured slower
+  // (17.9 against 20.6 us per iteration, profiles/r04/coarsest_barrier_variants.log).
+  // A compiler change could break the shipped order silently: the canaries are
+  // tests/test_gpu_parity.py test_fa_coarsest_level_production_horizon (1e5
+  // iterations against the oracle fixture) and test_fa_coarsest_level_shared_device,
+  // which must stay in the suite.
   constexpr bool rel = GE_BAR_ORDER == 1 || GE_BAR_ORDER == 2 || GE_BAR_ORDER == 4;
   constexpr int kRel = rel ? __ATOMIC_RELEASE : __ATOMIC_RELAXED;
   constexpr int kAR = rel ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
@@ -1740,10 +1748,16 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
   const bool packed_on = !(std::getenv("GE_FA_PACKED") && *std::getenv("GE_FA_PACKED") == '0');
   bool launched = false, fits = false, refused = false;
   DevBuf<int> bar;
-  // the start state, restored when the barrier times out
-  DevBuf<double> x0((size_t)n * D), f0((size_t)n * D);
-  GE_HIP(hipMemcpyAsync(x0.p, Xa, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
-  GE_HIP(hipMemcpyAsync(f0.p, pl->fprev.p, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+  // the start state, restored when the barrier times out: taken only once a fitting
+  // configuration is about to launch
+  DevBuf<double> x0, f0;
+  auto snapshot = [&] {
+    if (x0.p) return;
+    x0.alloc((size_t)n * D);
+    f0.alloc((size_t)n * D);
+    GE_HIP(hipMemcpyAsync(x0.p, Xa, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+    GE_HIP(hipMemcpyAsync(f0.p, pl->fprev.p, sizeof(double) * n * D, hipMemcpyDeviceToDevice, s));
+  };
   auto go = [&](auto GG) {
     constexpr int GC = decltype(GG)::value;
     const int nb = (n + kGrpT / GC - 1) / (kGrpT / GC);
@@ -1765,6 +1779,7 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
       GE_HIP(hipGetDevice(&dev));
       GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
       const long long limit = (long long)std::max(khz, 1000) * 2000;  // ~2 s per barrier
+      snapshot();
       bar.alloc(persist_bar_ints(nb));
       GE_HIP(hipMemsetAsync(bar.p, 0, sizeof(int) * bar.n, s));
       int n_ = n, it_ = iterations;
@@ -1948,6 +1963,10 @@ int ge_fa_plan_create(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d
     pl->c = ge::make_const(*p);
     try {
       ge::plan_init(pl);
+      // the symmetric path's tables now, not on the first step: that step may run on a
+      // caller's stream under graph capture (ge_ctx_set_stream), where sym_prepare's
+      // allocations and synchronisation are illegal
+      ge::sym_prepare(pl);
     } catch (...) {
       delete pl;
       throw;
@@ -2002,8 +2021,18 @@ int ge_fa_plan_kernel_ms(ge_fa_plan* pl, double* rep_ms, double* attr_ms, int* l
   });
 }
 
+// Waits for the plan's work; a symmetric launch whose hand-over wait timed out since
+// the last step is reported here (GE_ERR_STATE) instead of being lost.  The plan is
+// freed either way.
 int ge_fa_plan_destroy(ge_fa_plan* pl) {
-  return ge::guarded([&] { ge::plan_free(pl); });
+  return ge::guarded([&] {
+    if (!pl) return;
+    std::unique_ptr<ge_fa_plan> hold(pl);
+    if (pl->sym_err_h) {
+      GE_HIP(hipStreamSynchronize(pl->ctx->stream));
+      ge::sym_check(pl);
+    }
+  });
 }
 
 }  // extern "C"

@@ -779,7 +779,7 @@ __device__ void resolve_block(Dev d, int pass, int cidx) {
   int iters = 0;
   while (n > kLocalCand) {
     if (++iters > (1 << 22)) {  // cannot happen: the smallest live rank is taken every round
-      if (tid == 0) atomicExch(&d.cnt[C_OVF], 2);
+      if (tid == 0) atomicMax(&d.cnt[C_OVF], 2);
       return;
     }
     for (int c = tid; c < n; c += nt) {
@@ -1023,7 +1023,9 @@ __device__ void rebuild_list(const Dev& d, int u, Key* tk, W* tw, int mask, int 
       const int cap = count + count / 2 + 4;
       dst = (long long)atomicAdd(d.pool_top, (unsigned long long)cap);
       if (dst + cap > d.pool_cap) {
-        atomicExch(&d.cnt[C_OVF], 1);
+        // atomicMax: a resolve that did not converge earlier in the round (2, a bug)
+        // must not be masked by this capacity code (1, rerun on the host)
+        atomicMax(&d.cnt[C_OVF], 1);
         dst = -1;
       } else {
         d.aoff[u] = dst;
