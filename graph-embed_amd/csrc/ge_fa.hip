@@ -1657,8 +1657,6 @@ static void sym_check(ge_fa_plan* pl) {
   }
 }
 
-static void plan_free(ge_fa_plan* pl) { delete pl; }
-
 static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
   hipStream_t s = pl->ctx->stream;
   hipEvent_t* ev = nullptr;

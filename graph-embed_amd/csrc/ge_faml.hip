@@ -1016,6 +1016,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     auto scale_of = [&](int Tb) {
       return (est_prop ? (double)Tmax / Tb : 1.0) * (1.0 - big_first * Tb / Tmax);
     };
+    // row blocks' issue priority: one level per quarter of the longest row block's
+    // column tiles (ge_sym.hpp rows_prio; GE_FAML_ROWS_PRIO=0: all at priority 3)
+    int rows_q = 0;
+    for (size_t b = 0; b < big.size(); ++b)
+      if (as_rows[b]) rows_q = std::max(rows_q, (T[b] + 3) / 4);
+    for (int a : split) rows_q = std::max(rows_q, ((h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64 + 3) / 4);
+    if (const char* e = std::getenv("GE_FAML_ROWS_PRIO"); e && *e == '0') rows_q = 0;
     for (size_t b = 0; b < big.size(); ++b) {
       if (as_rows[b]) {
         // row blocks have no dependencies and each spans its aggregate's whole width:
@@ -1026,7 +1033,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         // no faster (N = 8 shares 26.6-28.0 against 27.0-27.3 ms per launch,
         // profiles/r05/scale_sim_c4_tailsplit.log) -- the share is bound by the row
         // blocks' instruction stream, not by the queue's last round.
-        for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, 0, T[b], kUnitRows, -1.0});
+        for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, rows_q, T[b], kUnitRows, -1.0});
         continue;
       }
       const double sc = scale_of(T[b]);
@@ -1037,7 +1044,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       int t0, t1;
       tiles_of(a, rank, t0, t1);
       const int Ta = (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64;
-      for (int A = t0; A < t1; ++A) us.push_back({a, A, 0, Ta, kUnitRows, -1.0});
+      for (int A = t0; A < t1; ++A) us.push_back({a, A, rows_q, Ta, kUnitRows, -1.0});
     }
     std::stable_sort(us.begin(), us.end(), [](const Unit& x, const Unit& y) {
       return x.est != y.est ? x.est < y.est : x.T > y.T;

@@ -256,30 +256,43 @@ __device__ __forceinline__ long long handover_wait(const int* flag, int A, int* 
   return STAMP ? rt_now() - t0 : 0;
 }
 
-// A row block: the 64 rows of tile A against the members [c0, c1) in ascending
-// order, every pair evaluated for its row (the plain ordered-pair scheme: no
-// dependencies besides the start value).  acc starts at +0 (fresh) or continues
-// the rows' sums passed in.  Used for whole aggregates whose sweep chain would
-// outlast the launch (c0 = 0, c1 = s) and for the cross-band parts of banded
-// aggregates (see faml_sym_repulse).
+// Issue priority of a row block with `rem` column tiles left: one level per
+// `quantum` tiles (capped at 3), so on each SIMD the wave with the most work left
+// issues first (longest remaining first).  Equal priorities fall back to the oldest
+// wave, which let one wave per SIMD run ahead through the queue while the other two
+// starved on the units they took at the start and finished last: on an N = 8 share
+// of C4 those units ran 15-25 ms against 5 ms, the launch's tail.
+__device__ __forceinline__ void rows_prio(int rem, int quantum) {
+  const int lv = quantum > 0 ? rem / quantum : 3;
+  if (lv >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (lv == 2) __builtin_amdgcn_s_setprio(2);
+  else if (lv == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
+// A row block: the 64 rows of tile A against all s members in ascending order,
+// every pair evaluated for its row (the plain ordered-pair scheme: no dependencies),
+// sums from +0, the rows' final sums to F.  Used for whole aggregates whose sweep
+// chain would outlast the launch (the shares of a multi-GPU run).  tile: 64
+// records of SymW<D> doubles in LDS.  quantum: see rows_prio (0: priority 3).
 template <int D, bool REPEL_ONE>
-__device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int c0, int c1,
-                                           bool fresh, const double* X, const double* DP,
-                                           double repel, bool repel_ok, double* tile,
-                                           double (&acc)[D]) {
+__device__ __forceinline__ void rows_block(int lane, int base, int s, int A, const double* X,
+                                           const double* DP, double repel, bool repel_ok,
+                                           double* tile, double* F, int quantum) {
   constexpr int WV = SymW<D>::v;
   const size_t rb = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
-  double xi[D], di = 1.0;
+  double xi[D], acc[D], di = 1.0;
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     xi[k] = rv ? X[(rb + lane) * D + k] : 0.0;
-    if (fresh) acc[k] = 0.0;
+    acc[k] = 0.0;
   }
   if (rv) di = DP[rb + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xi, di));
-  for (int j0 = c0; j0 < c1; j0 += 64) {
-    const int cnt = min(64, c1 - j0);
+  for (int j0 = 0; j0 < s; j0 += 64) {
+    const int cnt = min(64, s - j0);
+    rows_prio((s - j0) >> 6, quantum);
     wave_lds_sync();  // the previous tile has been read by every lane
     bool ok = true;
     if (lane < cnt) {
@@ -311,17 +324,8 @@ __device__ __forceinline__ void rows_range(int lane, int base, int s, int A, int
     }
   }
   wave_lds_sync();
-}
-
-// A whole row block (c0 = 0, c1 = s): the rows' final sums go to F.
-template <int D, bool REPEL_ONE>
-__device__ __forceinline__ void rows_block(int lane, int base, int s, int A, const double* X,
-                                           const double* DP, double repel, bool repel_ok,
-                                           double* tile, double* F) {
-  double acc[D];
-  rows_range<D, REPEL_ONE>(lane, base, s, A, 0, s, true, X, DP, repel, repel_ok, tile, acc);
-  if (64 * A + lane < s) {
-    const size_t rb = (size_t)base + 64 * (size_t)A;
+  __builtin_amdgcn_s_setprio(0);
+  if (rv) {
 #pragma unroll
     for (int k = 0; k < D; ++k) F[(rb + lane) * D + k] = acc[k];
   }
@@ -448,7 +452,8 @@ __device__ __forceinline__ void stamp_unit(long long* stamps, int qi, long long 
 // post row blocks), segmented row blocks and their round-5 tail split.
 constexpr int kUnitSweep = 0, kUnitRows = 1;
 
-// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog, kind}
+// units[q] = {aggregate, row tile A, offset of the aggregate's tiles in prog (a row
+// block: its priority quantum), kind}
 // in queue order; prog (ptiles progress counters) zeroed before the launch; queue =
 // one counter.  Every unit waits only on units before it in the queue.
 // 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
@@ -492,10 +497,9 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
     const size_t rb = (size_t)base + 64 * (size_t)A;
     if (u.w == kUnitRows) {
       // a row block spans its aggregate's whole width: the launch's critical path
-      // when the aggregate is large, so its wave takes issue priority on the SIMD
-      __builtin_amdgcn_s_setprio(3);
-      rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F);
-      __builtin_amdgcn_s_setprio(0);
+      // when the aggregate is large, so its wave takes issue priority over the
+      // sweeps on the SIMD, by the column tiles it has left (u.z: rows_prio's quantum)
+      rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F, u.z);
     } else {  // a sweep
       double racc[D];
       sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
