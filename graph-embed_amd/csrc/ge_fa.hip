@@ -841,6 +841,14 @@ __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
 // the acquire invalidate each cost more than the whole barrier's ordering is worth
 // here, so the shipped order is 0: agent-scope (L2-bypassing) stores and loads of
 // the coordinates, every store completed (s_waitcnt 0) before the arrival.
+// GE_DIAG_COARSE (diagnostics variants, scripts/build_variant.sh; wrong results): 1
+// packed rows skip their chunks, 2 also the staging -- what is left is the barrier,
+// the staging and the row update; 5 (right results) thread 0 of blocks 0, nb/2 and
+// nb-1 prints its microseconds per iteration in each phase at the end of the launch;
+// 6 (right results) as 5, with the adder's cycles of its adds alone.
+#ifndef GE_DIAG_COARSE
+#define GE_DIAG_COARSE 0
+#endif
 #ifndef GE_BAR_ORDER
 #define GE_BAR_ORDER 0
 #endif
@@ -1021,8 +1029,48 @@ __device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re
 constexpr int kPackR = kGrpT / 64;                     // rows per block
 constexpr int kPackU = 2;                               // terms per producer lane per chunk
 constexpr int kPackC = (kGrpT - 64) / kPackR * kPackU;  // partners per row per chunk (96)
+// Term-buffer line of one (row, dimension): kPackC terms + 2 doubles of padding, so the
+// adder lanes' 16-byte reads (one line each, same offset) fall in different LDS banks.
+// Unpadded (768-byte lines) all 12 lanes hit one bank: n = 998, the chunk loop took
+// 10.2 us per iteration (0.85 us per chunk of 96 partners) against ~0.3 us of adds.
+constexpr int kPackS = kPackC + 2;
 inline size_t packed_lds_bytes(int n, int D) {
-  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kPackR * D * kPackC);
+  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kPackR * D * kPackS);
+}
+
+// group_chain for the packed adder lane: the reads of batch b + 1 are issued before
+// the adds of batch b, so the LDS latency hides behind the dependent adds.  Same
+// order of additions (slots >= cnt add +0.0).
+template <int G>
+__device__ __forceinline__ double chain_prefetch(double a, const double* p, int cnt) {
+  constexpr int B = 16;
+  static_assert(G % B == 0, "batches of 16");
+  double v[2][B];
+#pragma unroll
+  for (int l = 0; l < B; l += 2) {
+    const double2 x = *reinterpret_cast<const double2*>(p + l);
+    v[0][l] = x.x;
+    v[0][l + 1] = x.y;
+  }
+#pragma unroll
+  for (int b = 0; b < G / B; ++b) {
+    if (b + 1 < G / B) {
+#pragma unroll
+      for (int l = 0; l < B; l += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(p + (b + 1) * B + l);
+        v[(b + 1) & 1][l] = x.x;
+        v[(b + 1) & 1][l + 1] = x.y;
+      }
+    }
+    if (cnt >= G) {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + v[b & 1][l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b & 1][l] : 0.0);
+    }
+  }
+  return a;
 }
 
 template <int D, bool REPEL_ONE, bool LINEAR, bool COH>
@@ -1033,21 +1081,27 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
                                                  const double* __restrict__ X,
                                                  const double* __restrict__ dp1, const FaConst& c,
                                                  double* __restrict__ Fprev,
-                                                 double* __restrict__ Xnext, double* smem) {
+                                                 double* __restrict__ Xnext, double* smem,
+                                                 long long* dt = nullptr) {
   static_assert(kPackR * D <= 64, "one adder lane per (row, dimension)");
-  static_assert(kPackC % 16 == 0, "group_chain reads batches of 16");
+  const long long tp0 = (GE_DIAG_COARSE >= 5 && dt) ? wall_clock64() : 0;
+  static_assert(kPackC % 16 == 0 && kPackS % 2 == 0, "chain_prefetch reads 16-byte pairs");
   constexpr int W = Rec<D>::W;
   constexpr int PL = kGrpT - 64;               // producer lanes
   constexpr int CL = PL / kPackR;              // producer lanes per row
-  constexpr int BUF = kPackR * D * kPackC;     // one half of the term buffer
+  constexpr int BUF = kPackR * D * kPackS;     // one half of the term buffer
   __shared__ int s_e[kPackR][2];
   double* rec = smem;
   double* tb = smem + (size_t)n * W;
   const int tid = threadIdx.x;
   const int r0 = rb + blk * kPackR;
+#if GE_DIAG_COARSE == 2  // diagnostics variant (wrong results): no staging
+  const bool ok = true;
+#else
   const bool ok =
       stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
       (REPEL_ONE || weight_ok(c.repel));
+#endif
   if (tid < kPackR) {
     const int i = r0 + tid;
     s_e[tid][0] = i < re ? ip[i] : 0;
@@ -1081,7 +1135,7 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
 #pragma unroll
     for (int u = 0; u < kPackU; ++u)
 #pragma unroll
-      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackC + pj + CL * u] = t[u][k];
+      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackS + pj + CL * u] = t[u][k];
   };
   const int pe0 = s_e[pr][0], pe1 = s_e[pr][1];
   auto att_chunk = [&](int ch, double* dst) {  // CSR entries e0 + ch * C + slot
@@ -1099,7 +1153,7 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
 #pragma unroll
     for (int u = 0; u < kPackU; ++u)
 #pragma unroll
-      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackC + pj + CL * u] = t[u][k];
+      for (int k = 0; k < D; ++k) dst[(pr * D + k) * kPackS + pj + CL * u] = t[u][k];
   };
   // adder lane: row ar, dimension ak
   const int ar = tid / D, ak = tid - ar * D;
@@ -1110,27 +1164,60 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
 #pragma unroll
   for (int r = 0; r < kPackR; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
   const int natt = (maxdeg + kPackC - 1) / kPackC;
+#if GE_DIAG_COARSE == 1 || GE_DIAG_COARSE == 2  // diagnostics (wrong results): no terms
+  const int ntot = 0;
+#else
   const int ntot = nrep + natt;  // the repulsion chunks, then the attraction chunks
+#endif
   const int adeg = adder ? s_e[ar][1] - s_e[ar][0] : 0;
+  const long long tp1 = (GE_DIAG_COARSE >= 5 && dt) ? wall_clock64() : 0;
   if (prod && ntot > 0) {
     if (nrep > 0) rep_chunk(0, tb);
     else att_chunk(0, tb);
   }
   __syncthreads();
+  long long busy = 0, busy_adds = 0;  // GE_DIAG_COARSE 5 / 6: clock64 cycles in the loop
   for (int ch = 0; ch < ntot; ++ch) {
     const double* cur = tb + (ch & 1) * BUF;
+    const long long tc0 = GE_DIAG_COARSE >= 5 ? clock64() : 0;
     if (tid < 64) {
       if (adder) {
         const int cnt = ch < nrep ? min(kPackC, n - ch * kPackC)
                                   : min(kPackC, max(0, adeg - (ch - nrep) * kPackC));
-        if (cnt > 0) a = group_chain<kPackC>(a, cur + (ar * D + ak) * kPackC, cnt);
+#if GE_DIAG_COARSE == 6  // diagnostics: every term in registers first, then the adds timed
+        if (cnt > 0) {
+          double v[kPackC];
+          const double* q = cur + (ar * D + ak) * kPackS;
+#pragma unroll
+          for (int l = 0; l < kPackC; ++l) v[l] = (l < cnt) ? q[l] : 0.0;
+          __builtin_amdgcn_s_waitcnt(0);
+          const long long ta = clock64();
+#pragma unroll
+          for (int l = 0; l < kPackC; ++l) a = a + v[l];
+          __asm__ volatile("" : "+v"(a));
+          busy_adds += clock64() - ta;
+        }
+#else
+        if (cnt > 0) a = chain_prefetch<kPackC>(a, cur + (ar * D + ak) * kPackS, cnt);
+#endif
       }
     } else if (ch + 1 < ntot) {
       double* nxt = tb + ((ch + 1) & 1) * BUF;
       if (ch + 1 < nrep) rep_chunk(ch + 1, nxt);
       else att_chunk(ch + 1 - nrep, nxt);
     }
+    if (GE_DIAG_COARSE >= 5) {
+      __builtin_amdgcn_s_waitcnt(0);
+      busy += clock64() - tc0;
+    }
     __syncthreads();
+  }
+  if (GE_DIAG_COARSE >= 5 && dt && (tid == 0 || tid == 64))
+    dt[tid == 0 ? 4 : 5] += (GE_DIAG_COARSE == 6 && tid == 0 ? busy_adds : busy) / max(ntot, 1);
+  if (GE_DIAG_COARSE >= 5 && dt && tid == 0) {
+    const long long tp2 = wall_clock64();
+    dt[0] += tp1 - tp0;  // staging
+    dt[1] += tp2 - tp1;  // chunks
   }
   if (tid < 64) {
     // the row's leader lane (r * D) gathers its dimensions, then gravity / update
@@ -1240,12 +1327,16 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
                       long long limit) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_ok;
+  long long dt[6] = {0, 0, 0, 0, 0, 0};  // GE_DIAG_COARSE 5: staging, chunks, rest, barrier,
+                                         // adder / producer cycles per chunk
+  long long tb0 = 0;
   for (int it = 0; it < iterations; ++it) {
     const double* X = (it & 1) ? Xb : Xa;
     double* Xn = (it & 1) ? Xa : Xb;
+    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) tb0 = wall_clock64();
     if constexpr (PACKED)
       packed_iteration<D, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
-                                                   Fprev, Xn, smem);
+                                                   Fprev, Xn, smem, dt);
     else
       grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1,
                                                        c, Fprev, Xn, smem);
@@ -1256,11 +1347,29 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
     __builtin_amdgcn_s_waitcnt(0);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __syncthreads();
+    long long tw = 0;
+    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) tw = wall_clock64();
     if (threadIdx.x == 0) s_ok = grid_arrive_wait(bar, gridDim.x, it, limit) ? 1 : 0;
     __syncthreads();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) {
+      const long long te = wall_clock64();
+      dt[2] += tw - tb0 - 0;  // the whole iteration before the barrier (minus the phases below)
+      dt[3] += te - tw;
+    }
     if (!s_ok) return;
   }
+  if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0 &&
+      (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1)) {
+    const double us = 0.01 / (iterations > 1 ? iterations - 1 : 1);  // 100 MHz ticks
+    printf("coarse diag block %d: staging %.2f chunks %.2f rest %.2f barrier %.2f us/iteration;"
+           " adder %lld cycles per chunk\n",
+           (int)blockIdx.x, dt[0] * us, dt[1] * us, (dt[2] - dt[0] - dt[1]) * us, dt[3] * us,
+           dt[4] / iterations);
+  }
+  if (GE_DIAG_COARSE >= 5 && threadIdx.x == 64 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+    printf("coarse diag block %d: producer wave %lld cycles per chunk\n", (int)blockIdx.x,
+           dt[5] / iterations);
 }
 
 // Mid-size levels (grouped_cap < n <= kStreamMax): the same fused iteration

@@ -1,6 +1,6 @@
 """Time a coarsest-level forceAtlas (1e5 iterations, src/embed.cpp:586) on a
 C4-coarsest-sized graph: the persistent launch against the per-iteration graph
-replay (GE_NO_PERSIST=1), same bits."""
+replay (GE_NO_PERSIST=1), same bits.  MODES=persistent,... picks the modes."""
 import os
 import sys
 import time
@@ -20,7 +20,7 @@ ctx = ge.Context()
 X0 = G.random_coords(n, 3, seed=1)
 ctx.force_atlas(A, 3, coords=X0, iterations=200)  # warm-up (module load, allocations)
 res = {}
-for mode in ("persistent", "persistent-nopack", "graph"):
+for mode in os.environ.get("MODES", "persistent,persistent-nopack,graph").split(","):
     if mode == "persistent-nopack":  # 64 lanes per row: one wave per row, not packed
         os.environ["GE_FA_PACKED"] = "0"
     if mode == "graph":
@@ -31,4 +31,4 @@ for mode in ("persistent", "persistent-nopack", "graph"):
     dt = time.perf_counter() - t
     print(f"{mode}: n={n} nnz={len(A[1])} iterations={its} {dt:.3f} s "
           f"({1e6 * dt / its:.2f} us/iteration)", flush=True)
-print("bit-identical:", all(np.array_equal(res["persistent"], r) for r in res.values()))
+print("bit-identical:", all(np.array_equal(next(iter(res.values())), r) for r in res.values()))
