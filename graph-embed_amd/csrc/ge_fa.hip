@@ -1038,36 +1038,43 @@ inline size_t packed_lds_bytes(int n, int D) {
   return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kPackR * D * kPackS);
 }
 
-// group_chain for the packed adder lane: the reads of batch b + 1 are issued before
-// the adds of batch b, so the LDS latency hides behind the dependent adds.  Same
-// order of additions (slots >= cnt add +0.0).
+// group_chain for the packed adder lane: the reads run GE_CHAIN_AHEAD batches (of 16
+// terms) ahead of the adds, so the LDS latency hides behind the dependent adds (3: n =
+// 998 18.2 us per iteration against 18.4 / 18.8 at 2 / 1).  The adder still takes ~20
+// cycles per add against 7 from registers and 11-12 from LDS in isolation
+// (scripts/micro/adder_chain.hip).  Same order of additions (slots >= cnt add +0.0).
+#ifndef GE_CHAIN_AHEAD
+#define GE_CHAIN_AHEAD 3
+#endif
 template <int G>
 __device__ __forceinline__ double chain_prefetch(double a, const double* p, int cnt) {
-  constexpr int B = 16;
+  constexpr int B = 16, NB = G / B, P = GE_CHAIN_AHEAD, R = P + 1;
   static_assert(G % B == 0, "batches of 16");
-  double v[2][B];
+  double v[R][B];
 #pragma unroll
-  for (int l = 0; l < B; l += 2) {
-    const double2 x = *reinterpret_cast<const double2*>(p + l);
-    v[0][l] = x.x;
-    v[0][l + 1] = x.y;
-  }
+  for (int b = 0; b < P && b < NB; ++b)
 #pragma unroll
-  for (int b = 0; b < G / B; ++b) {
-    if (b + 1 < G / B) {
+    for (int l = 0; l < B; l += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(p + b * B + l);
+      v[b][l] = x.x;
+      v[b][l + 1] = x.y;
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b + P < NB) {
 #pragma unroll
       for (int l = 0; l < B; l += 2) {
-        const double2 x = *reinterpret_cast<const double2*>(p + (b + 1) * B + l);
-        v[(b + 1) & 1][l] = x.x;
-        v[(b + 1) & 1][l + 1] = x.y;
+        const double2 x = *reinterpret_cast<const double2*>(p + (b + P) * B + l);
+        v[(b + P) % R][l] = x.x;
+        v[(b + P) % R][l + 1] = x.y;
       }
     }
     if (cnt >= G) {
 #pragma unroll
-      for (int l = 0; l < B; ++l) a = a + v[b & 1][l];
+      for (int l = 0; l < B; ++l) a = a + v[b % R][l];
     } else {
 #pragma unroll
-      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b & 1][l] : 0.0);
+      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b % R][l] : 0.0);
     }
   }
   return a;
@@ -1177,6 +1184,9 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
   }
   __syncthreads();
   long long busy = 0, busy_adds = 0;  // GE_DIAG_COARSE 5 / 6: clock64 cycles in the loop
+#ifdef GE_DIAG_ADDER_PRIO  // diagnostics variant: the adder wave at issue priority 3
+  if (tid < 64) __builtin_amdgcn_s_setprio(3);
+#endif
   for (int ch = 0; ch < ntot; ++ch) {
     const double* cur = tb + (ch & 1) * BUF;
     const long long tc0 = GE_DIAG_COARSE >= 5 ? clock64() : 0;
@@ -1212,6 +1222,9 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
     }
     __syncthreads();
   }
+#ifdef GE_DIAG_ADDER_PRIO
+  if (tid < 64) __builtin_amdgcn_s_setprio(0);
+#endif
   if (GE_DIAG_COARSE >= 5 && dt && (tid == 0 || tid == 64))
     dt[tid == 0 ? 4 : 5] += (GE_DIAG_COARSE == 6 && tid == 0 ? busy_adds : busy) / max(ntot, 1);
   if (GE_DIAG_COARSE >= 5 && dt && tid == 0) {
@@ -1363,13 +1376,13 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
       (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1)) {
     const double us = 0.01 / (iterations > 1 ? iterations - 1 : 1);  // 100 MHz ticks
     printf("coarse diag block %d: staging %.2f chunks %.2f rest %.2f barrier %.2f us/iteration;"
-           " adder %lld cycles per chunk\n",
+           " adder %lld cycles per chunk; HW_ID %x\n",
            (int)blockIdx.x, dt[0] * us, dt[1] * us, (dt[2] - dt[0] - dt[1]) * us, dt[3] * us,
-           dt[4] / iterations);
+           dt[4] / iterations, __builtin_amdgcn_s_getreg((31 << 11) | 4));
   }
   if (GE_DIAG_COARSE >= 5 && threadIdx.x == 64 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
-    printf("coarse diag block %d: producer wave %lld cycles per chunk\n", (int)blockIdx.x,
-           dt[5] / iterations);
+    printf("coarse diag block %d: producer wave %lld cycles per chunk; HW_ID %x\n", (int)blockIdx.x,
+           dt[5] / iterations, __builtin_amdgcn_s_getreg((31 << 11) | 4));
 }
 
 // Mid-size levels (grouped_cap < n <= kStreamMax): the same fused iteration
@@ -1871,8 +1884,11 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
     auto one = [&](auto RO, auto LI) {
       constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
       const bool pk = GC == 64 && packed_on;
-      const size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D))
-                            : grouped_lds_bytes(n, D);
+      size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D))
+                      : grouped_lds_bytes(n, D);
+#ifdef GE_DIAG_LDS_MIN  // diagnostics variant: LDS per block raised (fewer blocks per CU)
+      lds = std::max(lds, (size_t)GE_DIAG_LDS_MIN);
+#endif
       const void* fn =
           pk ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN, GC == 64>)
              : reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>);
