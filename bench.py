@@ -149,15 +149,17 @@ def cpu_share():
             share = min(share, max(1, int(int(quota) / int(period))))
     except (OSError, ValueError):
         pass
+    # the cgroup's cpuset, not /proc/self/status: that is the main thread's mask too
+    # (round 5's first cut read it and still reported 2)
     try:
-        with open("/proc/self/status") as f:
-            for line in f:
-                if line.startswith("Cpus_allowed_list"):
-                    n = 0
-                    for part in line.split(":", 1)[1].strip().split(","):
-                        a, _, b = part.partition("-")
-                        n += int(b or a) - int(a) + 1
-                    share = min(share, n)
+        with open("/sys/fs/cgroup/cpuset.cpus.effective") as f:
+            n = 0
+            for part in f.read().strip().split(","):
+                if part:
+                    a, _, b = part.partition("-")
+                    n += int(b or a) - int(a) + 1
+            if n > 0:
+                share = min(share, n)
     except (OSError, ValueError):
         pass
     return share

@@ -13,9 +13,10 @@
 // sweeps the columns j >= 64A in ascending order as a systolic array: at step
 // s lane l evaluates the pair (row 64A+l, column s-l), so
 //   * row l's own sum (lane register) receives its partners j > row in order;
-//   * column q's sum travels one lane per step (DPP wave shift), entering lane 0
-//     with the value the rows of earlier tiles left in F and collecting the rows
-//     of this tile in ascending order before it leaves lane 63 back to F.
+//   * column q's sum travels one lane per step (through its slot of the wave's LDS
+//     column ring: lane l + 1 reads at step s + 1 what lane l wrote at step s),
+//     entering lane 0 with the value the sweeps of earlier tiles handed over and
+//     collecting the rows of this tile in ascending order before it leaves lane 63.
 // In the diagonal tile, column q's travelling sum (partners < q of the tile,
 // after those of earlier tiles) reaches lane q exactly when that lane starts its
 // own row, and becomes the row's sum.  Row 64A+l therefore adds, in order:
@@ -44,16 +45,6 @@ template <int D>
 struct SymW {
   static constexpr int v = (D + 1 <= 4) ? 4 : 8;  // record: x[D], deg+1, pad
 };
-
-// Wave-wide shift by one lane (DPP wave_shr:1): lane l receives v of lane l-1,
-// lane 0 keeps in0 (no source lane: the DPP move leaves the destination alone).
-__device__ __forceinline__ double wave_shift_in(double v, double in0) {
-  const int lo = __builtin_amdgcn_update_dpp(__double2loint(in0), __double2loint(v), 0x138, 0xF,
-                                             0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(in0), __double2hiint(v), 0x138, 0xF,
-                                             0xF, false);
-  return __hiloint2double(hi, lo);
-}
 
 __device__ __forceinline__ double agent_ld(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
