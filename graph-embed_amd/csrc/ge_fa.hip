@@ -931,14 +931,16 @@ __device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re
                                                   const double* __restrict__ X,
                                                   const double* __restrict__ dp1, const FaConst& c,
                                                   double* __restrict__ Fprev,
-                                                  double* __restrict__ Xnext, double* smem) {
+                                                  double* __restrict__ Xnext, double* smem,
+                                                  int row0 = -1, int rend = 0x7fffffff) {
   constexpr int W = Rec<D>::W;
   double* rec = smem;
   double* tb = smem + (size_t)n * W;
   const int tid = threadIdx.x;
   const int g = tid % G;
-  const int i = rb + blk * (kGrpT / G) + tid / G;
-  const bool active = i < re;
+  // rows rb + blk * (kGrpT / G) + [0, kGrpT / G), or from row0 (below rend) when given
+  const int i = (row0 >= 0 ? row0 : rb + blk * (kGrpT / G)) + tid / G;
+  const bool active = i < min(re, rend);
   const bool ok =
       stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
       (REPEL_ONE || weight_ok(c.repel));
@@ -1026,16 +1028,18 @@ __device__ __forceinline__ void grouped_iteration(int blk, int n, int rb, int re
 // the bits are those of grouped_iteration.  In-domain blocks only: a block whose
 // records leave the exact-division domain runs grouped_iteration<G = 64> (the same
 // rows) instead.
-constexpr int kPackR = kGrpT / 64;                     // rows per block
-constexpr int kPackU = 2;                               // terms per producer lane per chunk
-constexpr int kPackC = (kGrpT - 64) / kPackR * kPackU;  // partners per row per chunk (96)
+// R rows per block (4, or 6 when 4 would need more blocks than CUs: C4's coarsest level
+// has n = 1 068 = 267 blocks of 4 on 256 CUs, and a CU holding two blocks slows the
+// whole grid): 192 / R producer lanes per row, each evaluating kPackC R / 192 partners
+// of a chunk.
+constexpr int kPackC = 96;  // partners per row per chunk
 // Term-buffer line of one (row, dimension): kPackC terms + 2 doubles of padding, so the
 // adder lanes' 16-byte reads (one line each, same offset) fall in different LDS banks.
 // Unpadded (768-byte lines) all 12 lanes hit one bank: n = 998, the chunk loop took
 // 10.2 us per iteration (0.85 us per chunk of 96 partners) against ~0.3 us of adds.
 constexpr int kPackS = kPackC + 2;
-inline size_t packed_lds_bytes(int n, int D) {
-  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * kPackR * D * kPackS);
+inline size_t packed_lds_bytes(int n, int D, int R) {
+  return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * (size_t)R * D * kPackS);
 }
 
 // group_chain for the packed adder lane: the reads run GE_CHAIN_AHEAD batches (of 16
@@ -1080,7 +1084,7 @@ __device__ __forceinline__ double chain_prefetch(double a, const double* p, int 
   return a;
 }
 
-template <int D, bool REPEL_ONE, bool LINEAR, bool COH>
+template <int D, bool REPEL_ONE, bool LINEAR, bool COH, int R>
 __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
                                                  const int* __restrict__ ip,
                                                  const int* __restrict__ ix,
@@ -1090,18 +1094,20 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
                                                  double* __restrict__ Fprev,
                                                  double* __restrict__ Xnext, double* smem,
                                                  long long* dt = nullptr) {
-  static_assert(kPackR * D <= 64, "one adder lane per (row, dimension)");
+  static_assert(R * D <= 64, "one adder lane per (row, dimension)");
   const long long tp0 = (GE_DIAG_COARSE >= 5 && dt) ? wall_clock64() : 0;
   static_assert(kPackC % 16 == 0 && kPackS % 2 == 0, "chain_prefetch reads 16-byte pairs");
   constexpr int W = Rec<D>::W;
   constexpr int PL = kGrpT - 64;               // producer lanes
-  constexpr int CL = PL / kPackR;              // producer lanes per row
-  constexpr int BUF = kPackR * D * kPackS;     // one half of the term buffer
-  __shared__ int s_e[kPackR][2];
+  constexpr int CL = PL / R;                   // producer lanes per row
+  constexpr int kPackU = kPackC / CL;          // terms per producer lane per chunk
+  static_assert(CL * R == PL && kPackU * CL == kPackC, "producer lanes tile the chunk");
+  constexpr int BUF = R * D * kPackS;          // one half of the term buffer
+  __shared__ int s_e[R][2];
   double* rec = smem;
   double* tb = smem + (size_t)n * W;
   const int tid = threadIdx.x;
-  const int r0 = rb + blk * kPackR;
+  const int r0 = rb + blk * R;
 #if GE_DIAG_COARSE == 2  // diagnostics variant (wrong results): no staging
   const bool ok = true;
 #else
@@ -1109,14 +1115,15 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
       stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
       (REPEL_ONE || weight_ok(c.repel));
 #endif
-  if (tid < kPackR) {
+  if (tid < R) {
     const int i = r0 + tid;
     s_e[tid][0] = i < re ? ip[i] : 0;
     s_e[tid][1] = i < re ? ip[i + 1] : 0;
   }
   if (!__syncthreads_and(ok)) {  // block-uniform: the general bodies, same rows
-    grouped_iteration<D, 64, REPEL_ONE, LINEAR, COH>(blk, n, rb, re, ip, ix, dx, X, dp1, c, Fprev,
-                                                     Xnext, smem);
+    for (int q = 0; q < R; q += kGrpT / 64)  // kGrpT / 64 rows per call
+      grouped_iteration<D, 64, REPEL_ONE, LINEAR, COH>(blk, n, rb, re, ip, ix, dx, X, dp1, c,
+                                                       Fprev, Xnext, smem, r0 + q, r0 + R);
     return;
   }
   // producer lane: row pr, chunk slots pj + CL * u
@@ -1164,12 +1171,12 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
   };
   // adder lane: row ar, dimension ak
   const int ar = tid / D, ak = tid - ar * D;
-  const bool adder = tid < kPackR * D;
+  const bool adder = tid < R * D;
   double a = 0.0;
   const int nrep = (n + kPackC - 1) / kPackC;
   int maxdeg = 0;
 #pragma unroll
-  for (int r = 0; r < kPackR; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
+  for (int r = 0; r < R; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
   const int natt = (maxdeg + kPackC - 1) / kPackC;
 #if GE_DIAG_COARSE == 1 || GE_DIAG_COARSE == 2  // diagnostics (wrong results): no terms
   const int ntot = 0;
@@ -1331,7 +1338,7 @@ __device__ bool grid_arrive_wait(int* bar, int nb, int it, long long limit) {
   return true;
 }
 
-template <int D, int G, bool REPEL_ONE, bool LINEAR, bool PACKED = false>
+template <int D, int G, bool REPEL_ONE, bool LINEAR, int PACKED = 0>  // PACKED: rows per block
 __global__ void __launch_bounds__(kGrpT)
 fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__ ix,
                       const double* __restrict__ dx, double* __restrict__ Xa,
@@ -1347,8 +1354,8 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
     const double* X = (it & 1) ? Xb : Xa;
     double* Xn = (it & 1) ? Xa : Xb;
     if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) tb0 = wall_clock64();
-    if constexpr (PACKED)
-      packed_iteration<D, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
+    if constexpr (PACKED > 0)
+      packed_iteration<D, REPEL_ONE, LINEAR, true, PACKED>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
                                                    Fprev, Xn, smem, dt);
     else
       grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1,
@@ -1884,26 +1891,34 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
     auto one = [&](auto RO, auto LI) {
       constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
       const bool pk = GC == 64 && packed_on;
-      size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D))
+      // packed rows per block: 6 where blocks of 4 would outnumber the CUs (n = 1 068 at
+      // C4: 178 blocks of 6 against 267 of 4; GE_FA_PACK_ROWS=4|6 overrides, tuning)
+      int R = pk ? ((n + 3) / 4 > pl->cus ? 6 : 4) : 0;
+      if (const char* e = std::getenv("GE_FA_PACK_ROWS"); pk && e) R = std::atoi(e) == 6 ? 6 : 4;
+      const int nbk = pk ? (n + R - 1) / R : nb;
+      size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D, R))
                       : grouped_lds_bytes(n, D);
 #ifdef GE_DIAG_LDS_MIN  // diagnostics variant: LDS per block raised (fewer blocks per CU)
       lds = std::max(lds, (size_t)GE_DIAG_LDS_MIN);
 #endif
       const void* fn =
-          pk ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN, GC == 64>)
-             : reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>);
+          !pk    ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>)
+          : R == 6 ? reinterpret_cast<const void*>(
+                         &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 6 : 0>)
+                   : reinterpret_cast<const void*>(
+                         &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 4 : 0>);
       if (lds > 65536)
         GE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       int occ = 0;
       GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kGrpT, lds));
-      if ((long long)nb > (long long)occ * pl->cus) return;  // the whole grid resident
+      if ((long long)nbk > (long long)occ * pl->cus) return;  // the whole grid resident
       fits = true;
       int dev = 0, khz = 0;
       GE_HIP(hipGetDevice(&dev));
       GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
       const long long limit = (long long)std::max(khz, 1000) * 2000;  // ~2 s per barrier
       snapshot();
-      bar.alloc(persist_bar_ints(nb));
+      bar.alloc(persist_bar_ints(nbk));
       GE_HIP(hipMemsetAsync(bar.p, 0, sizeof(int) * bar.n, s));
       int n_ = n, it_ = iterations;
       long long lim_ = limit;
@@ -1915,7 +1930,7 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
       double* fp_ = pl->fprev.p;
       int* bar_ = bar.p;
       void* args[] = {&n_, &ip_, &ix_, &dx_, &Xa, &Xb, &dp_, &c_, &fp_, &bar_, &it_, &lim_};
-      const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(nb), dim3(kGrpT), args,
+      const hipError_t e = hipLaunchCooperativeKernel(fn, dim3(nbk), dim3(kGrpT), args,
                                                       (unsigned)lds, s);
       if (e == hipErrorCooperativeLaunchTooLarge) {
         (void)hipGetLastError();

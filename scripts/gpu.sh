@@ -17,8 +17,8 @@
 #                                                            -> pmc_<CTRS>_W.csv (+ summary)
 #   c5[:ARGS]        scripts/c5_attraction.py [ARGS]  (configs[4] attraction pass)
 #                                                            -> c5_attraction.json
-#   pmc5:CTRS        one --pmc pass over c5_attraction.py (2 passes + 1 warmup),
-#                    attraction kernels only             -> pmc_<CTRS>_c5.csv (+ summary)
+#   pmc5:CTRS[:ARGS] one --pmc pass over c5_attraction.py (2 passes + 1 warmup) [ARGS,
+#                    commas = spaces], attraction kernels only -> pmc_<CTRS>[_args]_c5.csv
 #   py:SCRIPT[:ARGS] python -u SCRIPT [ARGS, commas = spaces] -> SCRIPT-name.log
 #   env:K=V          export K=V for the following steps
 set -o pipefail
@@ -72,10 +72,10 @@ for step in "$@"; do
         2> $OUT/c5_attraction.err || fail "$step" $? $OUT/c5_attraction.err
       cat $OUT/c5_attraction.json ;;
     pmc5)
-      name=${a//,/_}
+      name=${a//,/_}${b:+_${b//[^a-z0-9]/}}
       timeout -s KILL 600 rocprofv3 --pmc ${a//,/ } --kernel-include-regex "rows_kernel|heavy_" \
         --output-format csv -d $OUT/pmc5_$name -o p -- python3 scripts/c5_attraction.py --steps 2 \
-        --warmup 1 > $OUT/pmc_${name}_c5.log 2>&1 || fail "$step" $? $OUT/pmc_${name}_c5.log
+        --warmup 1 ${b//,/ } > $OUT/pmc_${name}_c5.log 2>&1 || fail "$step" $? $OUT/pmc_${name}_c5.log
       cp "$(find $OUT/pmc5_$name -name '*counter_collection.csv' | head -1)" $OUT/pmc_${name}_c5.csv
       rm -rf $OUT/pmc5_$name
       python3 scripts/pmc_summary.py $OUT/pmc_${name}_c5.csv "" > $OUT/pmc_${name}_c5.txt 2>&1

@@ -263,17 +263,21 @@ def test_fa_small_level_graph_replay(ctx, oracle):
                                             (1300, 4, "0", 128), (2900, 3, "32", 129),
                                             (1068, 3, "16", 140), (500, 1, "64", 257),
                                             (1068, 3, "nopack", 131), (97, 4, "0", 129),
-                                            (1999, 2, "0", 128)])
+                                            (1999, 2, "0", 128), (700, 3, "pack6", 131),
+                                            (1068, 3, "pack4", 129), (1300, 1, "pack6", 128)])
 def test_fa_persistent_small_level(ctx, oracle, monkeypatch, n, dim, grp, its):
     """Small levels with >= 128 iterations run every iteration in one launch
     (fa_grouped_persistent: resident blocks, grid barrier, coordinates in two
     alternating buffers); odd and even counts, G lanes per row.  At 64 lanes per
     row the rows are packed (packed_iteration: one adder wave, three producer
     waves; ragged last block, rows of degree above one chunk); "nopack" keeps one
-    wave per row."""
+    wave per row; "pack4" / "pack6" force 4 / 6 packed rows per block (6 is the
+    default once blocks of 4 would outnumber the CUs, n > 1024)."""
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
     if grp == "nopack":
         monkeypatch.setenv("GE_FA_PACKED", "0")
+    elif grp.startswith("pack"):
+        monkeypatch.setenv("GE_FA_PACK_ROWS", grp[4:])
     elif grp != "0":
         monkeypatch.setenv("GE_GRP_G", grp)
     A = G.rmat(n, 6 * n, seed=n + dim)
@@ -320,7 +324,7 @@ def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("grp", ["0", "nopack", "16", "32"])
+@pytest.mark.parametrize("grp", ["0", "nopack", "16", "32", "pack4"])
 def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     """The coarsest level at its production size and horizon: an R-MAT LCC coarsened
     twice by partition(A, 0.125) (n = 1067, integer weights, self-loops), seeded
@@ -330,6 +334,8 @@ def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
     if grp == "nopack":  # 64 lanes per row, one wave per row (grouped_iteration)
         monkeypatch.setenv("GE_FA_PACKED", "0")
+    elif grp == "pack4":  # 4 packed rows per block (n = 1067: the default is 6)
+        monkeypatch.setenv("GE_FA_PACK_ROWS", "4")
     elif grp != "0":
         monkeypatch.setenv("GE_GRP_G", grp)
     g = golden("fa_coarsest_1e5")
