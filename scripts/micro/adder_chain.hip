@@ -44,6 +44,67 @@ __device__ __forceinline__ double chain_interleaved(double a, const double* p) {
   return a;
 }
 
+// the shipped form (ge_fa.hip chain_prefetch): three batches ahead, runtime cnt
+__device__ __forceinline__ double chain_shipped(double a, const double* p, int cnt) {
+  constexpr int NB = C / B, P = 3, R = P + 1;
+  double v[R][B];
+#pragma unroll
+  for (int b = 0; b < P && b < NB; ++b)
+#pragma unroll
+    for (int l = 0; l < B; l += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(p + b * B + l);
+      v[b][l] = x.x;
+      v[b][l + 1] = x.y;
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b + P < NB) {
+#pragma unroll
+      for (int l = 0; l < B; l += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(p + (b + P) * B + l);
+        v[(b + P) % R][l] = x.x;
+        v[(b + P) % R][l + 1] = x.y;
+      }
+    }
+    if (cnt >= C) {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + v[b % R][l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b % R][l] : 0.0);
+    }
+  }
+  return a;
+}
+
+// the round-5 fix: no per-batch branch on the count (full chunks: plain adds)
+__device__ __forceinline__ double chain_fixed(double a, const double* p) {
+  constexpr int NB = C / B, P = 3, R = P + 1;
+  double v[R][B];
+#pragma unroll
+  for (int b = 0; b < P && b < NB; ++b)
+#pragma unroll
+    for (int l = 0; l < B; l += 2) {
+      const double2 x = *reinterpret_cast<const double2*>(p + b * B + l);
+      v[b][l] = x.x;
+      v[b][l + 1] = x.y;
+    }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b + P < NB) {
+#pragma unroll
+      for (int l = 0; l < B; l += 2) {
+        const double2 x = *reinterpret_cast<const double2*>(p + (b + P) * B + l);
+        v[(b + P) % R][l] = x.x;
+        v[(b + P) % R][l + 1] = x.y;
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < B; ++l) a = a + v[b % R][l];
+  }
+  return a;
+}
+
 __device__ __forceinline__ double chain_prefetch(double a, const double* p) {
   double v[2][B];
 #pragma unroll
@@ -70,7 +131,9 @@ __device__ __forceinline__ double chain_prefetch(double a, const double* p) {
 
 // MODE 0: registers only; 1: LDS, no barrier; 2: LDS + __syncthreads per chunk;
 // 3: as 2 with waves 1-3 running 200 fp64 FMAs per chunk; 4: as 2, reads interleaved;
-// 5: as 2 with waves 1-3 reading records and writing terms to LDS like the producers
+// 5: as 2 with waves 1-3 reading records and writing terms to LDS like the producers;
+// 6: as 5 with the round-5 adder before the fix (three batches ahead, a per-lane count
+// tested per batch); 7: as 6 without the count (the fix: full chunks add plainly)
 template <int MODE>
 __global__ void adder(const double* in, double* out, int chunks, long long* cyc) {
   __shared__ __attribute__((aligned(16))) double buf[2][12 * S];
@@ -91,6 +154,10 @@ __global__ void adder(const double* in, double* out, int chunks, long long* cyc)
         for (int l = 0; l < C; ++l) a = a + r;
       } else if (MODE == 4) {
         a = chain_interleaved(a, &buf[ch & 1][tid * S]);
+      } else if (MODE == 7) {
+        a = chain_fixed(a, &buf[ch & 1][tid * S]);
+      } else if (MODE == 6) {
+        a = chain_shipped(a, &buf[ch & 1][tid * S], chunks > 1 ? C - (ch == chunks - 1) : 1);
       } else {
         a = chain_prefetch(a, &buf[ch & 1][tid * S]);
       }
@@ -98,7 +165,7 @@ __global__ void adder(const double* in, double* out, int chunks, long long* cyc)
       for (int k = 0; k < 25; ++k)
 #pragma unroll
         for (int u = 0; u < 8; ++u) w[u] = __builtin_fma(w[u], r, 1e-3);
-    } else if (MODE == 5 && tid >= 64) {  // producer-like: 2 records in, 6 terms out, fp64 work
+    } else if (MODE >= 5 && tid >= 64) {  // producer-like: 2 records in, 6 terms out, fp64 work
       const int p = tid - 64, pr = p / 48, pj = p % 48;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -127,10 +194,11 @@ int main() {
   hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice);
   const int chunks = 4096;
   long long c;
-  const char* names[6] = {"registers", "LDS prefetched", "LDS + barrier", "LDS + barrier + 3 busy waves",
-                          "LDS interleaved + barrier", "LDS + barrier + producer-like"};
+  const char* names[8] = {"registers", "LDS prefetched", "LDS + barrier", "LDS + barrier + 3 busy waves",
+                          "LDS interleaved + barrier", "LDS + barrier + producer-like",
+                          "shipped chain + producer-like", "fixed chain + producer-like"};
   for (int rep = 0; rep < 2; ++rep) {
-    for (int m = 0; m < 6; ++m) {
+    for (int m = 0; m < 8; ++m) {
       switch (m) {
         case 0: hipLaunchKernelGGL(adder<0>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
         case 1: hipLaunchKernelGGL(adder<1>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
@@ -138,6 +206,8 @@ int main() {
         case 3: hipLaunchKernelGGL(adder<3>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
         case 4: hipLaunchKernelGGL(adder<4>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
         case 5: hipLaunchKernelGGL(adder<5>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
+        case 6: hipLaunchKernelGGL(adder<6>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
+        case 7: hipLaunchKernelGGL(adder<7>, dim3(1), dim3(256), 0, 0, in, out, chunks, cyc); break;
       }
       hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
       if (rep == 1) printf("%-30s %.0f cycles per chunk of %d adds (%.2f per add)\n", names[m],
