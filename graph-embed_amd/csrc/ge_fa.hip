@@ -1050,7 +1050,7 @@ inline size_t packed_lds_bytes(int n, int D, int R) {
 #ifndef GE_CHAIN_AHEAD
 #define GE_CHAIN_AHEAD 3
 #endif
-template <int G, bool FULL>
+template <int G>
 __device__ __forceinline__ double chain_prefetch(double a, const double* p, int cnt) {
   constexpr int B = 16, NB = G / B, P = GE_CHAIN_AHEAD, R = P + 1;
   static_assert(G % B == 0, "batches of 16");
@@ -1073,12 +1073,13 @@ __device__ __forceinline__ double chain_prefetch(double a, const double* p, int 
         v[(b + P) % R][l + 1] = x.y;
       }
     }
-    // FULL (a wave-uniform full chunk): plain adds; otherwise every slot >= cnt is
-    // selected to +0.0 -- branch-free: a per-lane `cnt >= G` test per batch made the
-    // compiler split every batch into two exec-masked paths, which doubled the adder's
-    // time per add (scripts/micro/adder_chain.hip: 26 against 13 cycles)
+    if (cnt >= G) {
 #pragma unroll
-    for (int l = 0; l < B; ++l) a = a + ((FULL || b * B + l < cnt) ? v[b % R][l] : 0.0);
+      for (int l = 0; l < B; ++l) a = a + v[b % R][l];
+    } else {
+#pragma unroll
+      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b % R][l] : 0.0);
+    }
   }
   return a;
 }
@@ -1214,10 +1215,7 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
           busy_adds += clock64() - ta;
         }
 #else
-        if ((ch + 1) * kPackC <= n)  // a full repulsion chunk: wave-uniform
-          a = chain_prefetch<kPackC, true>(a, cur + (ar * D + ak) * kPackS, cnt);
-        else if (cnt > 0)
-          a = chain_prefetch<kPackC, false>(a, cur + (ar * D + ak) * kPackS, cnt);
+        if (cnt > 0) a = chain_prefetch<kPackC>(a, cur + (ar * D + ak) * kPackS, cnt);
 #endif
       }
     } else if (ch + 1 < ntot) {
