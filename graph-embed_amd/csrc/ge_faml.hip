@@ -1018,11 +1018,13 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     };
     // row blocks' issue priority: one level per quarter of the longest row block's
     // column tiles (ge_sym.hpp rows_prio; GE_FAML_ROWS_PRIO=0: all at priority 3)
-    int rows_q = 0;
+    // (GE_FAML_ROWS_PRIO=k: one level per 1/k of it instead, tuning)
+    int rows_q = 0, prio_div = 4;
+    if (const char* e = std::getenv("GE_FAML_ROWS_PRIO")) prio_div = std::atoi(e);
     for (size_t b = 0; b < big.size(); ++b)
-      if (as_rows[b]) rows_q = std::max(rows_q, (T[b] + 3) / 4);
-    for (int a : split) rows_q = std::max(rows_q, ((h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64 + 3) / 4);
-    if (const char* e = std::getenv("GE_FAML_ROWS_PRIO"); e && *e == '0') rows_q = 0;
+      if (as_rows[b]) rows_q = std::max(rows_q, T[b]);
+    for (int a : split) rows_q = std::max(rows_q, (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64);
+    rows_q = prio_div > 0 ? (rows_q + prio_div - 1) / prio_div : 0;
     for (size_t b = 0; b < big.size(); ++b) {
       if (as_rows[b]) {
         // row blocks have no dependencies and each spans its aggregate's whole width:
