@@ -598,9 +598,12 @@ class FamlPlan:
         return dict(zip(("sweeps", "banded", "row_blocks", "units"), (x.value for x in v)))
 
     def close(self):
+        """Destroys the plan; raises GeError when the library reports a failure
+        that surfaced only at teardown (e.g. a sweep hand-over wait that timed out
+        after the last step).  __del__ swallows it."""
         if self.h:
-            lib().ge_faml_plan_destroy(self.h)
-            self.h = None
+            h, self.h = self.h, None
+            _check(lib().ge_faml_plan_destroy(h))
 
     def __del__(self):
         try:
@@ -639,9 +642,12 @@ class FaPlan:
         return a.value, b.value, c.value
 
     def close(self):
+        """Destroys the plan; raises GeError when the library reports a failure
+        that surfaced only at teardown (e.g. a sweep hand-over wait that timed out
+        after the last step).  __del__ swallows it."""
         if self.h:
-            lib().ge_fa_plan_destroy(self.h)
-            self.h = None
+            h, self.h = self.h, None
+            _check(lib().ge_fa_plan_destroy(h))
 
     def __del__(self):
         try:

@@ -115,6 +115,49 @@ def test_c4_level0_sampled_aggregates(ctx, oracle, heartbeat):
     assert np.isfinite(got).all()
 
 
+def test_c4_level0_oracle_at_embed_horizon(ctx, golden, monkeypatch, heartbeat):
+    """configs[3] (C4) level 0 at the embed's own horizon, 100 iterations
+    (src/embed.cpp:793), against the oracle's 100 iterations
+    (tests/golden/make_c4_level0_100.py; 1 301 s on 8 threads) on the largest aggregate
+    (41 930 members: the longest sweep chain), the two smallest streamed and the two
+    largest LDS-resident aggregates (the size-class boundary) and 100 random small
+    ones.  The shipped schedule (symmetric sweeps) and the register-flow sweeps
+    (GE_SYM_FLOW=1, every streamed aggregate as sweeps) must both equal the oracle
+    bit for bit."""
+    import hashlib
+    import time
+    t0 = time.perf_counter()
+    g = golden("faml_c4_level0_100it")
+    L = ge.largest_component(ge.rmat_csr(10_000_000, 80_000_000, seed=12345))
+    PT = ctx.partition(L, 0.125)[0]
+    _progress(t0, "C4 device partition")
+    lvl0 = hashlib.sha256(np.ascontiguousarray(PT[0], np.int32).tobytes() +
+                          np.ascontiguousarray(PT[1], np.int32).tobytes()).hexdigest()
+    assert lvl0 == str(g["level0_sha256"])
+    aggs = g["aggs"]
+    h = hashlib.sha256()
+    for a in aggs:
+        h.update(np.ascontiguousarray(PT[1][PT[0][a]:PT[0][a + 1]], np.int32).tobytes())
+    assert h.hexdigest() == str(g["members_sha256"])
+    m = PT[2]
+    vA = ge.vertex_of(PT)
+    cA = ge.uniform_stream(7, m * 3).reshape(m, 3)
+    rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
+    rows = g["rows"].astype(np.int64)
+    assert np.diff(PT[0])[aggs].max() == 41930
+    for name, env in (("shipped", {}), ("flow", {"GE_SYM_FLOW": "1", "GE_FAML_SYM_CHAIN": "0"})):
+        for k in ("GE_SYM_FLOW", "GE_FAML_SYM_CHAIN"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with heartbeat(f"C4 level 0, 100 iterations, {name}"):
+            got = ctx.force_atlas_ml(L, PT, vA, cA, rA, 3, iterations=int(g["iterations"]),
+                                     seed=int(g["seed"]))
+        _progress(t0, f"C4 {name} done")
+        assert np.isfinite(got).all()
+        assert np.array_equal(got[rows], g["x"]), name
+
+
 def test_c4_level0_schedules_agree_at_embed_horizon(ctx, monkeypatch, heartbeat):
     """C4 level 0 over the embed's 100 iterations (src/embed.cpp:793): the streamed
     aggregates (98 at C4, up to 41 930 members) as symmetric sweeps (the default), as

@@ -286,10 +286,16 @@ def test_fa_persistent_small_level(ctx, oracle, monkeypatch, n, dim, grp, its):
     assert np.array_equal(ctx.force_atlas(A, dim, coords=X0, iterations=its), want)
 
 
-def test_fa_persistent_params_and_domain(ctx, oracle, monkeypatch):
+@pytest.mark.parametrize("pack", ["default", "4", "6"])
+def test_fa_persistent_params_and_domain(ctx, oracle, monkeypatch, pack):
     """Non-default parameters (repel != 1, weights off) and a start outside the
-    exact-division domain (the general bodies) in the persistent kernel."""
+    exact-division domain (the general bodies) in the persistent kernel.  With 6
+    packed rows per block an out-of-domain block runs the general body twice over
+    explicit row windows (rows r0..r0+3, then r0+4..r0+5; ge_fa.hip
+    packed_iteration), so both packings are forced here."""
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
+    if pack != "default":
+        monkeypatch.setenv("GE_FA_PACK_ROWS", pack)
     A = G.largest_component(G.rmat(600, 3000, seed=8))
     n = len(A[0]) - 1
     X0 = G.random_coords(n, 3, seed=5)

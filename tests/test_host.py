@@ -153,6 +153,38 @@ def test_device_entry_points_fail_loudly_without_gpu():
         ge.Context(0)
 
 
+def test_plan_close_reports_teardown_errors(monkeypatch):
+    """ge_fa_plan_destroy / ge_faml_plan_destroy return GE_ERR_STATE when a sweep
+    hand-over wait timed out after the last step (ge_fa.hip sym_check): close()
+    raises it, __del__ swallows it.  The library is replaced by a stub whose
+    destroy calls fail, so no device is needed."""
+    class Stub:
+        def __init__(self):
+            self.destroyed = []
+
+        def ge_fa_plan_destroy(self, h):
+            self.destroyed.append(h)
+            return 4
+
+        ge_faml_plan_destroy = ge_fa_plan_destroy
+
+        def ge_last_error(self):
+            return b"symmetric hand-over wait timed out"
+
+    stub = Stub()
+    monkeypatch.setattr(ge, "_lib", stub)
+    for cls in (ge.FaPlan, ge.FamlPlan):
+        plan = cls.__new__(cls)
+        plan.h = 1234
+        with pytest.raises(ge.GeError, match="hand-over"):
+            plan.close()
+        assert plan.h is None
+        plan.close()  # a second close is a no-op
+        plan.h = 99
+        plan.__del__()  # swallowed
+    assert stub.destroyed == [1234, 99, 1234, 99]
+
+
 @pytest.mark.parametrize("dim,init", [(2, True), (3, True), (4, False), (3, False)])
 def test_embed_via_minimization(oracle, dim, init):
     """ge_embed_via_minimization (host C++, directions on OpenMP threads) against
