@@ -1815,8 +1815,7 @@ static void plan_step(ge_fa_plan* pl, const double* xc, double* xn) {
       GE_HIP(hipMemsetAsync(pl->ctl.p, 0, sizeof(int) * pl->ctl.n, s));
       sym_repulse_launch(D, pl->sym_blocks, s, pl->sym_units, pl->units.p, pl->ctl.p,
                          pl->seg.p, xc, pl->dp1.p, pl->p.repel, pl->frep.p, pl->hand.p,
-                         (size_t)pl->n, pl->ctl.p + 1, pl->sym_err_d, pl->sym_limit,
-                         sym_flow_env() == 1);
+                         (size_t)pl->n, pl->ctl.p + 1, pl->sym_err_d, pl->sym_limit);
     } else {
       launch_repulsion<D>(s, pl->p.mode, pl->n, pl->rb, pl->re, xc, pl->dp1.p, pl->p.repel,
                           pl->frep.p, pl->fpart.p, pl->cus);

@@ -734,7 +734,6 @@ struct ge_faml_plan {
   long long sym_limit = 0;  // that wait's bound in ticks of the device wall clock
   int nunits = 0, ntiles = 0, sym_blocks = 0;
   int rows_mode = 0, swept = 0;  // streamed aggregates by schedule (ge_sym.hpp)
-  bool sym_flow = false;         // register-flow sweeps (ge_sym.hpp FLOW)
   std::vector<int4> h_units;          // host copy of `units` (timeline dumps)
   ge::DevBuf<long long> stamps;       // GE_SYM_STAMPS: per-unit timeline of the last launch
   std::string stamp_path;
@@ -986,7 +985,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
                    "predicted %.1f tile-times\n",
                    big.size(), *std::max_element(T.begin(), T.end()), waves, nr, best);
     }
-    pl->sym_flow = sym_flow_env() == 1;
     pl->rows_mode = pl->swept = 0;
     for (size_t b = 0; b < big.size(); ++b) {
       if (as_rows[b]) ++pl->rows_mode;
@@ -1244,11 +1242,6 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);
 #endif
-          } else if (!pl->stamp_path.empty() && pl->sym_flow) {
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false, true>),
-                               dim3(pl->sym_blocks), dim3(kSymT), 0, ss, pl->nunits, pl->units.p,
-                               pl->queue.p + it, pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H,
-                               hs, pl->prog.p, err, lim, pl->stamps.p);
           } else if (!pl->stamp_path.empty()) {
             hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
@@ -1257,7 +1250,7 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           } else {
             sym_repulse_launch(D, pl->sym_blocks, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim, pl->sym_flow);
+                               err, lim);
           }
         } else {
           launch_big_repulse<D>(pl->code, pl->rep_blocks, ss, pl->nitems, pl->items.p,
@@ -1324,18 +1317,10 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
                         double repel, double* F, double* H, size_t hs, int* prog, int* err,
-                        long long limit, bool flow) {
+                        long long limit) {
   dispatch_dim(dim, [&](auto Dc) {
     constexpr int D = decltype(Dc)::value;
-    if (flow && repel == 1.0)
-      hipLaunchKernelGGL((faml_sym_repulse<D, true, false, false, true>), dim3(blocks), dim3(kSymT),
-                         0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit,
-                         nullptr);
-    else if (flow)
-      hipLaunchKernelGGL((faml_sym_repulse<D, false, false, false, true>), dim3(blocks),
-                         dim3(kSymT), 0, s, nunits, units, queue, seg, X, DP, repel, F, H, hs, prog,
-                         err, limit, nullptr);
-    else if (repel == 1.0)
+    if (repel == 1.0)
       hipLaunchKernelGGL((faml_sym_repulse<D, true>), dim3(blocks), dim3(kSymT), 0, s, nunits,
                          units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
     else
@@ -1343,11 +1328,6 @@ void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const in
                          units, queue, seg, X, DP, repel, F, H, hs, prog, err, limit, nullptr);
   });
   GE_HIP(hipGetLastError());
-}
-
-int sym_flow_env() {
-  const char* e = std::getenv("GE_SYM_FLOW");
-  return e && *e ? (*e == '0' ? 0 : 1) : -1;
 }
 
 // Blocks per CU of a single-level symmetric launch (one aggregate of n / 64 row

@@ -164,11 +164,8 @@ void check_csr(int n, const int* ip, const int* ix, const double* dx);
 void sym_repulse_launch(int dim, int blocks, hipStream_t s, int nunits, const int4* units,
                         int* queue, const int* seg, const double* X, const double* DP,
                         double repel, double* F, double* H, size_t hs, int* prog, int* err,
-                        long long limit, bool flow = false);
+                        long long limit);
 int sym_blocks_per_cu(int dim);
-// Register-flow sweeps (ge_sym.hpp FLOW): GE_SYM_FLOW=1 forces them, =0 forbids them;
-// returns -1 when unset (the plan decides).
-int sym_flow_env();
 
 void fa_run_device(ge_ctx* ctx, int n, int nnz, const int* d_ip, const int* d_ix,
                    const double* d_dx, int dim, double* d_x, int iterations,

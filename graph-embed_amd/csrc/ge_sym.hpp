@@ -173,119 +173,6 @@ __device__ __forceinline__ void tile_steps_any(int tt, int lane, const double* r
     tile_steps<D, REPEL_ONE, true>(tt, lane, rec, col, xr, dr, repel, racc);
 }
 
-// ---- Register-flow sweeps (round 6): the column sums travel in registers.
-//
-// A lone LDS-ring sweep is latency-bound: each step's column read waits for the
-// previous step's write (the compiler barrier keeps the next step's record reads
-// behind it too), so a step costs the whole dependent chain of its term (~600
-// cycles) and a column tile ~16.5 us on an otherwise idle SIMD, against ~6 us of
-// issue.  That is the tile-time of a sweep chain, and chains bound the shares of a
-// multi-GPU run.  Here the column sums move one lane per step by a DPP wave shift
-// (lane 0 takes the entering sum, lane 63's leaving sum is stored to the ring), so
-// nothing but the register chain orders the steps, and the terms of B consecutive
-// steps are evaluated before their adds: B independent instruction chains.  Same
-// operations on the same operands as the LDS ring (each column receives the rows
-// in ascending lane order, each row its partners in ascending order), so the same
-// bits; ~6 more VALU per step (the shift), more registers.
-
-// Wave-wide shift by one lane (DPP wave_shr:1): lane l receives v of lane l-1,
-// lane 0 keeps in0 (no source lane: the DPP move leaves the destination alone).
-__device__ __forceinline__ double wave_shift_in(double v, double in0) {
-  const int lo = __builtin_amdgcn_update_dpp(__double2loint(in0), __double2loint(v), 0x138, 0xF,
-                                             0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(in0), __double2hiint(v), 0x138, 0xF,
-                                             0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// One register-flow step at any position (col_step's counterpart): column sg
-// enters lane 0 from its ring slot, column sg - 63 leaves lane 63 into its slot.
-template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void flow_step(int sg, int lane, const double* rec, double* col,
-                                          const double (&xr)[D], double dr, double repel,
-                                          double (&racc)[D], double (&flow)[D]) {
-  const int q = sg - lane;
-  const int p = q & (kSymRing - 1);
-  double xq[D + 1];
-#pragma unroll
-  for (int k = 0; k <= D; ++k) xq[k] = rec[k * kRecSlots + p];
-#pragma unroll
-  for (int k = 0; k < D; ++k) flow[k] = wave_shift_in(flow[k], col[k * kSymRing + (sg & (kSymRing - 1))]);
-  if (DIAG && q == lane) {  // column q = this lane's row: its sum so far is the row's
-#pragma unroll
-    for (int k = 0; k < D; ++k) racc[k] = flow[k];
-  }
-  double t[D];
-  rep_term<D, SHARED, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
-  if (!SHARED && DIAG && q == lane) {  // the `/` form skips the self pair (ge_pair.hpp)
-#pragma unroll
-    for (int k = 0; k < D; ++k) t[k] = 0.0;
-  }
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    racc[k] = racc[k] + t[k];
-    flow[k] = flow[k] - t[k];
-  }
-  if (lane == 63) {  // column sg - 63 is complete
-    const int po = (sg - 63) & (kSymRing - 1);
-#pragma unroll
-    for (int k = 0; k < D; ++k) col[k * kSymRing + po] = flow[k];
-  }
-}
-
-template <int D, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void flow_steps(bool fast, int s0, int s1, int lane, const double* rec,
-                                           double* col, const double (&xr)[D], double dr,
-                                           double repel, double (&racc)[D], double (&flow)[D]) {
-  if (fast)
-    for (int sg = s0; sg < s1; ++sg)
-      flow_step<D, true, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc, flow);
-  else
-    for (int sg = s0; sg < s1; ++sg)
-      flow_step<D, false, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc, flow);
-}
-
-// The 64 steps of a full column tile tt >= 2 in the shared-reciprocal domain, B
-// steps per batch: the B terms first (independent), then the ordered row adds and
-// column shifts, then lane 63 stores the B columns that left it (one branch per
-// batch).  Records at immediate offsets as in tile_steps; the entering sums are
-// uniform (broadcast) reads of the tile's staged slots.
-template <int D, bool REPEL_ONE, int B>
-__device__ __forceinline__ void flow_tile_steps(int tt, int lane, const double* rec, double* col,
-                                                const double (&xr)[D], double dr, double repel,
-                                                double (&racc)[D], double (&flow)[D]) {
-  static_assert(64 % B == 0, "batches tile the 64 steps");
-  const double* rb = rec + ((64 * tt - lane) & (kSymRing - 1));
-  const double* ib = col + ((64 * tt) & (kSymRing - 1));
-  for (int j0 = 0; j0 < 64; j0 += B) {
-    double t[B][D], fl[B][D];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-      double xq[D + 1];
-#pragma unroll
-      for (int k = 0; k <= D; ++k) xq[k] = rb[k * kRecSlots + j0 + b];
-      rep_term<D, true, REPEL_ONE>(xr, xq, dr, xq[D], repel, t[b]);
-    }
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        racc[k] = racc[k] + t[b][k];
-        flow[k] = wave_shift_in(flow[k], ib[k * kSymRing + j0 + b]) - t[b][k];
-        fl[b][k] = flow[k];
-      }
-    }
-    if (lane == 63) {
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        const int po = (64 * tt + j0 + b - 63) & (kSymRing - 1);
-#pragma unroll
-        for (int k = 0; k < D; ++k) col[k * kSymRing + po] = fl[b][k];
-      }
-    }
-  }
-}
-
 // Hand-over slot of member c, dimension k: component-major H[k * hs + c].
 template <int D>
 __device__ __forceinline__ double* hand_at(double* H, size_t hs, size_t c, int k) {
@@ -445,8 +332,7 @@ constexpr int kStampWords = 8;
 // One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
 // column sums handed to the next sweep tile by tile.  rec / col: this wave's rings
 // (see kSymRing).  STAMP: spin ticks and the first hand-over time.
-// FLOW: register-flow steps (flow_*, B steps per batch) instead of the LDS ring.
-template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false, bool FLOW = false, int B = 4>
+template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false>
 __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
                                            const double* __restrict__ X,
                                            const double* __restrict__ DP, double repel,
@@ -458,26 +344,18 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   const size_t cbase = (size_t)base + 64 * (size_t)A;
   const bool rv = 64 * A + lane < s;
   double xr[D], racc[D], dr = 0.0;  // a row past the aggregate is inert
-  double flow[D];  // FLOW: the column sum at this lane (dead until a column reaches it)
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     xr[k] = rv ? X[(cbase + lane) * D + k] : 0.0;
     racc[k] = 0.0;
-    flow[k] = 0.0;
   }
   if (rv) dr = DP[cbase + lane];
   const bool rows_ok = repel_ok && __all(!rv || vertex_ok<D>(xr, dr));
   const int ncols = s - 64 * A;
   const int ntiles = (ncols + 63) >> 6;
   bool ok_prev = true;
-  // FLOW: tile tt + 1's column records, and its entering sums when its hand-over has
-  // already arrived, are loaded while tile tt computes (their memory round trips
-  // leave the sweep's chain)
-  double nx[D], nh[D], nd = 0.0;
-  bool nh_ok = false;
   for (int tt = 0; tt < ntiles; ++tt) {
-    const bool pre = FLOW && tt > 0;
-    if (A > 0 && !NOWAIT && !(pre && nh_ok)) {  // sweeps 0..A-1 wrote column tile A + tt back
+    if (A > 0 && !NOWAIT) {  // the sweeps 0..A-1 have written column tile A + tt back
       const long long w = handover_wait<STAMP>(tprog + tt, A, err, limit, give_up);
       if (STAMP) {
         spin += w;
@@ -493,16 +371,10 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     double xc[D], ic[D], dc = 0.0;  // a column past the aggregate is inert
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-      if (pre) {
-        xc[k] = nx[k];
-        ic[k] = nh_ok ? nh[k] : ((cv && A > 0) ? agent_ld(hand_at<D>(H, hs, cbase + qc, k)) : 0.0);
-      } else {
-        xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
-        ic[k] = (cv && A > 0) ? agent_ld(hand_at<D>(H, hs, cbase + qc, k)) : 0.0;
-      }
+      xc[k] = cv ? X[(cbase + qc) * D + k] : 0.0;
+      ic[k] = (cv && A > 0) ? agent_ld(hand_at<D>(H, hs, cbase + qc, k)) : 0.0;
     }
-    if (pre) dc = nd;
-    else if (cv) dc = DP[cbase + qc];
+    if (cv) dc = DP[cbase + qc];
     const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
     const int p = qc & (kSymRing - 1);
 #pragma unroll
@@ -516,32 +388,10 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
       for (int k = 0; k < D; ++k) rec[k * kRecSlots + p + kSymRing] = xc[k];
       rec[D * kRecSlots + p + kSymRing] = dc;
     }
-    if (FLOW && tt + 1 < ntiles) {
-      const bool cn = qc + 64 < ncols;
-#pragma unroll
-      for (int k = 0; k < D; ++k) nx[k] = cn ? X[(cbase + qc + 64) * D + k] : 0.0;
-      nd = cn ? DP[cbase + qc + 64] : 0.0;
-      nh_ok = A == 0 || NOWAIT || (!give_up && seen(tprog + tt + 1) >= A);
-      if (nh_ok) {
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-          nh[k] = (cn && A > 0) ? agent_ld(hand_at<D>(H, hs, cbase + qc + 64, k)) : 0.0;
-      }
-    }
     wave_lds_sync();
     // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
     const bool fast = rows_ok && ok_cur && ok_prev;
-    if (FLOW) {
-      if (tt < 2)
-        flow_steps<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
-                                       racc, flow);
-      else if (fast)
-        flow_tile_steps<D, REPEL_ONE, B>(tt, lane, rec, col, xr, dr, repel, racc, flow);
-      else
-        flow_steps<D, REPEL_ONE, false>(false, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr,
-                                        repel, racc, flow);
-    } else if (tt < 2)
+    if (tt < 2)
       col_steps<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
                                     racc);
     else if (fast)
@@ -563,14 +413,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     wave_lds_sync();
   }
   const int s0 = 64 * ntiles, s1 = ncols + 63;
-  if (FLOW) {
-    if (ntiles < 2)
-      flow_steps<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel,
-                                     racc, flow);
-    else
-      flow_steps<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel,
-                                      racc, flow);
-  } else if (ntiles < 2)
+  if (ntiles < 2)
     col_steps<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel, racc);
   else
     col_steps<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel,
@@ -613,10 +456,8 @@ constexpr int kUnitSweep = 0, kUnitRows = 1;
 // resident kernels were locked out until the repulsion launches ended and ran
 // during the attraction passes instead (C4: 4.44 against 3.52 ms per pass, 140.4
 // against 137.0-137.3 ms per step; profiles/r04/ab_rows_r03.log).
-// FLOW (round 6): register-flow sweeps (flow_tile_steps), for launches whose sweep
-// chains bound them; three waves per SIMD (<= 168 VGPRs).
-template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false, bool FLOW = false>
-__global__ void __launch_bounds__(kSymT, FLOW ? 3 : 4)
+template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
+__global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
                  const double* __restrict__ DP, double repel, double* __restrict__ F,
@@ -652,7 +493,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F, u.z);
     } else {  // a sweep
       double racc[D];
-      sweep_unit<D, REPEL_ONE, STAMP, NOWAIT, FLOW>(lane, A, base, s, prog + u.z + A, X, DP, repel,
+      sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, col,
                                               spin, t_first, racc);
       if (64 * A + lane < s) {

@@ -121,9 +121,9 @@ def test_c4_level0_oracle_at_embed_horizon(ctx, golden, monkeypatch, heartbeat):
     (tests/golden/make_c4_level0_100.py; 1 301 s on 8 threads) on the largest aggregate
     (41 930 members: the longest sweep chain), the two smallest streamed and the two
     largest LDS-resident aggregates (the size-class boundary) and 100 random small
-    ones.  The shipped schedule (symmetric sweeps) and the register-flow sweeps
-    (GE_SYM_FLOW=1, every streamed aggregate as sweeps) must both equal the oracle
-    bit for bit."""
+    ones.  The shipped schedule (symmetric sweeps at N = 1) and every streamed
+    aggregate as ordered row blocks (the multi-GPU shares' schedule,
+    GE_FAML_SYM_CHAIN=1e9) must both equal the oracle bit for bit."""
     import hashlib
     import time
     t0 = time.perf_counter()
@@ -145,8 +145,8 @@ def test_c4_level0_oracle_at_embed_horizon(ctx, golden, monkeypatch, heartbeat):
     rA = 0.01 + 0.19 * (ge.uniform_stream(8, m) + 1.0) / 2.0
     rows = g["rows"].astype(np.int64)
     assert np.diff(PT[0])[aggs].max() == 41930
-    for name, env in (("shipped", {}), ("flow", {"GE_SYM_FLOW": "1", "GE_FAML_SYM_CHAIN": "0"})):
-        for k in ("GE_SYM_FLOW", "GE_FAML_SYM_CHAIN"):
+    for name, env in (("shipped", {}), ("row_blocks", {"GE_FAML_SYM_CHAIN": "1e9"})):
+        for k in ("GE_FAML_SYM_CHAIN",):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
