@@ -730,6 +730,8 @@ struct RoundExport {
   int* hcnt = nullptr;  // nullptr: not the round's last pass
   unsigned long long* htop = nullptr;
   int* hrec = nullptr;
+  int* hseq = nullptr;  // the round number, written last (the host spins on it)
+  int seq = 0;
   int spec = 0;
 };
 
@@ -742,6 +744,11 @@ __device__ void export_round(const Dev& d, const RoundExport& ex) {
   const int* src = reinterpret_cast<const int*>(d.mrec);
   for (int w = t; w < nw; w += blockDim.x)
     __hip_atomic_store(&ex.hrec[w], src[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // every thread's stores are complete at the system level before the round number
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(ex.hseq, ex.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The matching's last kernel of a pass; then the pass's list counters are zeroed
@@ -1468,7 +1475,6 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   DevBuf<int> gkey(gcap);
   DevBuf<double> gw(gcap);
   DevBuf<unsigned long long> tops(2);  // [0] pool top, [1] global-table top
-  DevBuf<int2> d_changes(n / 2 + 1);
   DevBuf<int2> pairs(kPairCap), pinfo(n);
   DevBuf<int> pcnt(n), pbuf(kPairCap), t2arg(n), t2arg2(n);
   DevBuf<double> t2w(n), t2b2(n), t2w2(n), t2b3(n);
@@ -1644,13 +1650,17 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     unsigned long long* p;
     ~PinnedTop() { (void)hipHostFree(p); }
   } pinned_top{h_top};
+  int* h_seq = nullptr;  // the last exported round (RoundExport::hseq)
+  GE_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_seq), sizeof(int)));
+  *h_seq = 0;
+  struct PinnedSeq {
+    int* p;
+    ~PinnedSeq() { (void)hipHostFree(p); }
+  } pinned_seq{h_seq};
 
   int alist_len = n;
   int mid_blocks = 1024;  // GE_PART_MID_BLOCKS: tuning
   if (const char* e = std::getenv("GE_PART_MID_BLOCKS")) mid_blocks = std::max(1, std::atoi(e));
-  // GE_PART_BLIT_EXPORT=1: the round's counts and records by three blit copies
-  // (the earlier path, for comparison) instead of the export by the last resolve_kernel
-  const bool blit_export = std::getenv("GE_PART_BLIT_EXPORT") != nullptr;
   const int spec = std::min(kSpecMerges, n / 2 + 1);
   double t_dev = 0, t_host = 0, t_compact = 0;
   long long total_merges = 0;
@@ -1661,20 +1671,32 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
   long long stat[NCNT] = {0};
   int rstat[NCNT] = {0};  // this round's list sizes (GE_PROFILE_ROUNDS)
   const bool prof_rounds = prof && std::getenv("GE_PROFILE_ROUNDS");
+  // A pass is its scans (classify_scan .. filter: they read lists, alphas and the
+  // touched flags, never the rank array) and its resolve (the greedy matching in
+  // `used` order: reads the rank array).  Round r + 1's first scans are queued right
+  // behind round r's contraction, before the host's swap-pop of round r, and round
+  // r's rank update behind them: the device runs the scans while the host does the
+  // order-dependent bookkeeping (round 6: it waited for it before, 0.53 s at C4 in
+  // gaps before rank_update_kernel and classify_scan_kernel,
+  // profiles/r06/partition_c4_gaps_start.txt).
+  auto launch_scans = [&](int pass, int round) {
+    hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
+                       pass, alist_len, round, round == 1 ? 1 : 0, pass == matching - 1 ? 1 : 0);
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
+    hipLaunchKernelGGL(scan_mid_kernel, dim3(mid_blocks), dim3(256), 0, st, d, pass);
+    hipLaunchKernelGGL(scan_big_kernel<256>, dim3(1024), dim3(256), 0, st, d, pass);
+    hipLaunchKernelGGL(scan_huge_part_kernel, dim3(kHugeChunks, 64), dim3(1024), 0, st, d, pass,
+                       hpart.p, hcap);
+    hipLaunchKernelGGL(scan_huge_final_kernel, dim3(64), dim3(256), 0, st, d, pass, hpart.p, hcap);
+    hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
+  };
+  bool scans_queued = false;  // pass 0's scans of the coming round are already queued
   do {
     std::fill(rstat, rstat + NCNT, 0);
     ++rounds;
     const auto t0 = now();
     for (int pass = 0; pass < matching; ++pass) {
-      hipLaunchKernelGGL(classify_scan_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st, d,
-                         pass, alist_len, rounds, rounds == 1 ? 1 : 0, pass == matching - 1 ? 1 : 0);
-      hipLaunchKernelGGL(scan_small_kernel, dim3(1024), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_mid_kernel, dim3(mid_blocks), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_big_kernel<256>, dim3(1024), dim3(256), 0, st, d, pass);
-      hipLaunchKernelGGL(scan_huge_part_kernel, dim3(kHugeChunks, 64), dim3(1024), 0, st, d, pass,
-                         hpart.p, hcap);
-      hipLaunchKernelGGL(scan_huge_final_kernel, dim3(64), dim3(256), 0, st, d, pass, hpart.p, hcap);
-      hipLaunchKernelGGL(filter_kernel, dim3(1024), dim3(256), 0, st, d);
+      if (!(pass == 0 && scans_queued)) launch_scans(pass, rounds);
       hipLaunchKernelGGL(resolve_min_kernel, dim3(512), dim3(256), 0, st, d);
       hipLaunchKernelGGL(resolve_select_kernel, dim3(512), dim3(256), 0, st, d, pass);
       hipLaunchKernelGGL(resolve_filter_kernel, dim3(512), dim3(256), 0, st, d);
@@ -1682,11 +1704,13 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         Dev d2 = d;  // the survivors are in cand2
         std::swap(d2.cand, d2.cand2);
         RoundExport ex;  // the round's last pass exports its counts and records
-        if (pass == matching - 1 && !blit_export) {
+        if (pass == matching - 1) {
           ex.tops = tops.p;
           ex.hcnt = h_cnt;
           ex.htop = h_top;
           ex.hrec = reinterpret_cast<int*>(h_mrec);
+          ex.hseq = h_seq;
+          ex.seq = rounds;
           ex.spec = spec;
         }
         hipLaunchKernelGGL(resolve_kernel, dim3(1), dim3(1024), 0, st, d2, pass, (int)C_CAND2, ex);
@@ -1702,14 +1726,22 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         }
       }
     }
-    // the merge records of a typical round come with the counts (one synchronisation)
-    if (blit_export) {
-      GE_HIP(hipMemcpyAsync(h_cnt, cnt.p, sizeof(int) * NCNT, hipMemcpyDeviceToHost, st));
-      GE_HIP(hipMemcpyAsync(h_top, tops.p, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-      GE_HIP(hipMemcpyAsync(h_mrec, mrec.p, sizeof(MergeRec) * spec, hipMemcpyDeviceToHost, st));
-    }
     GE_HIP(hipGetLastError());
-    GE_HIP(hipStreamSynchronize(st));
+    // The round's last resolve_kernel writes its counts and the first `spec` merge
+    // records into pinned memory and then the round number into *h_seq (system-scope
+    // release): the host spins on it instead of a stream synchronisation, whose
+    // wake-up cost ~25 us per round (0.26 s at C4 in the gap before merge_apply_kernel).
+    // A stream that finished or failed without writing it ends the spin (the error
+    // is then reported by the synchronisation).
+    for (long long spins = 1;; ++spins) {
+      if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == rounds) break;
+      if ((spins & 1023) == 0 && hipStreamQuery(st) != hipErrorNotReady) {
+        GE_HIP(hipStreamSynchronize(st));
+        if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) != rounds)
+          throw Error(GE_ERR_STATE, "partition_device: a round ended without its export");
+        break;
+      }
+    }
     if (rounds <= 2) note("round: matching passes done");
     rb.merges = h_cnt[C_MERGE];
     if (prof) {
@@ -1776,6 +1808,22 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
         note("round: contraction done");
       }
     }
+    M_prev = M;
+    M -= nm;  // the swap-pop below removes nm entries of `used`
+    const bool more = 1.0 * M / M_prev < stall;  // :1838
+    if (more) {
+      if (alist_len > M + M / 4 + 1024) {  // drop the dead entries of the alive list
+        GE_HIP(hipMemsetAsync(cnt.p + C_ALIVE2, 0, sizeof(int), st));
+        hipLaunchKernelGGL(alive_compact_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st,
+                           d, alist_len);
+        GE_HIP(hipGetLastError());
+        std::swap(d.alist, d.alist2);
+        alist_len = M;
+      }
+      launch_scans(0, rounds + 1);  // the next round's first scans (no rank reads)
+      GE_HIP(hipGetLastError());
+      scans_queued = true;
+    }
     const auto t1 = now();
     t_dev += secs(t0, t1);
     // ---- host: merges in the reference's order (pass, then `used` slot)
@@ -1786,11 +1834,13 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     double dQ = 0.0;
     for (const auto& m : order) dQ += m.eta;  // :1749
     Q += dQ;                                  // :1784
-    M_prev = M;
-    if (1.0 * M / N <= cf) {  // :1797-1815 (before this round's swap-pop)
+    if (1.0 * M_prev / N <= cf) {  // :1797-1815 (before this round's swap-pop)
+      const int M_now = M;
+      M = M_prev;  // snap() reads the pre-round count
       snap();
+      M = M_now;
       basis = used;
-      N = M;
+      N = M_prev;
     }
     int nch = 0;
     for (const auto& m : order) {  // :1819-1834
@@ -1800,7 +1850,6 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
       used.pop_back();
       pointer[last] = idx;
       id[m.gone] = m.keep;
-      --M;
       if (stamp[last] != rounds) {  // a vertex may move several times: upload its final slot
         stamp[last] = rounds;
         moved[nch++] = last;
@@ -1808,25 +1857,12 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
     }
     for (int x = 0; x < nch; ++x) h_changes[x] = make_int2(moved[x], pointer[moved[x]]);
     total_merges += nm;
-    if (nch > 0) {
+    if (nch > 0 && more) {
       // the kernel reads the pinned changes directly (no H2D blit); the host next
-      // writes h_changes after the next round's synchronisation, past this kernel
-      const int2* chg = h_changes;
-      if (blit_export) {
-        GE_HIP(hipMemcpyAsync(d_changes.p, h_changes, sizeof(int2) * nch, hipMemcpyHostToDevice, st));
-        chg = d_changes.p;
-      }
+      // writes h_changes after the next round's export, past this kernel
       hipLaunchKernelGGL(rank_update_kernel, dim3(blocks_for(nch, 256)), dim3(256), 0, st, d, nch,
-                         chg);
+                         (const int2*)h_changes);
       GE_HIP(hipGetLastError());
-    }
-    if (alist_len > M + M / 4 + 1024) {  // drop the dead entries of the alive list
-      GE_HIP(hipMemsetAsync(cnt.p + C_ALIVE2, 0, sizeof(int), st));
-      hipLaunchKernelGGL(alive_compact_kernel, dim3(blocks_for(alist_len, 256)), dim3(256), 0, st,
-                         d, alist_len);
-      GE_HIP(hipGetLastError());
-      std::swap(d.alist, d.alist2);
-      alist_len = M;
     }
     t_host += secs(t1, now());
     if (progress && (rounds <= 3 || secs(t_last_note, now()) > 10.0)) {
@@ -1843,7 +1879,8 @@ ge_hier* partition_device(ge_ctx* ctx, int n, const int* I, const int* J, const 
                    rstat[C_HUGE], rstat[C_PROP], rstat[C_CAND], rstat[C_DIRTY], rstat[C_W],
                    rstat[C_B], rstat[C_G], rstat[C_PATCH], rstat[C_PF_SHORT], rstat[C_PF_SIZE],
                    rstat[C_PF_FIT]);
-  } while (1.0 * M / M_prev < stall);  // :1838
+    if (!more) break;
+  } while (true);
   GE_HIP(hipStreamSynchronize(st));
   snap();  // :1840-1852
   if (prof)

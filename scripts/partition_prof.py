@@ -1,11 +1,15 @@
 """Device partition of a configs[] graph with the library's own phase timers
 (GE_PROFILE_PARTITION: device rounds / host bookkeeping / compactions, list
-sizes) and progress notes; CFG=c4 (default) or c5."""
+sizes) and progress notes; CFG=c4 (default) or c5; PROF=0: without the phase
+timers (they synchronise after every pass)."""
 import os
 import sys
 import time
 
-os.environ.setdefault("GE_PROFILE_PARTITION", "1")
+if os.environ.get("PROF") == "0":  # plain timing: no per-pass synchronisations
+    os.environ.pop("GE_PROFILE_PARTITION", None)
+else:
+    os.environ.setdefault("GE_PROFILE_PARTITION", "1")
 os.environ.setdefault("GE_PROGRESS", "1")
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "graph-embed_amd", "py"))
