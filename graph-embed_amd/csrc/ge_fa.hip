@@ -1745,8 +1745,10 @@ static void plan_init(ge_fa_plan* pl) {
   // removed in round 5)
 }
 
-// The symmetric path's units, progress counters and hand-over buffer (n x d), made
-// on the plan's first step (a plan used only for its row kernels never needs them).
+// The symmetric path's units, progress counters and hand-over buffer (n x d).  Made
+// when the plan is created (ge_fa_plan_create, and before any graph capture in
+// fa_run_device), so every symmetric plan holds them, one used only for
+// ge_fa_plan_attract included; the step's call is a no-op then.
 static void sym_prepare(ge_fa_plan* pl) {
   if (!pl->sym || pl->sym_units > 0) return;
   hipStream_t s = pl->ctx->stream;

@@ -1039,6 +1039,8 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
         continue;
       }
       const double sc = scale_of(T[b]);
+      // (round 6 measured sweep issue priorities by the followers a sweep holds up:
+      // 115.8-116.0 against 115.3-115.4 ms per launch, profiles/r06/ab_sym_prio.log)
       for (int A = 0; A < T[b]; ++A) us.push_back({big[b], A, pb, T[b], kUnitSweep, est_k * A * sc});
       pb += T[b];
     }

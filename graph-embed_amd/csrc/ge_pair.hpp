@@ -74,7 +74,7 @@ __device__ __forceinline__ double attraction_mag(double dis, double a, double di
 // within ~2^-80 of a rounding boundary, and a y off by one ulp changes the quotient
 // only where n / d lies within ~2^-106 of one: the same bits as `/` except with
 // probability ~2^-80 per division (ge_selftest.hip compares every term with the
-// rcp path and with `/` on 2^28 pairs per call, tests/test_gpu_parity.py).  Two
+// rcp path and with `/` on 2^30 draws per test call, tests/test_gpu_parity.py).  Two
 // quarter-rate v_rcp_f64 and two FMAs fewer per pair than rcp-based reciprocals.
 struct PairDen {
   double dis;

@@ -56,43 +56,61 @@ __device__ __forceinline__ void agent_st(double* p, double v) {
 __device__ __forceinline__ long long rt_now() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
 // LDS of one sweep wave (round 5).  Column q of the sweep (q = column - 64 A) keeps
-// its running sum in LDS, in slot q & 127 of the column ring `col` (D components, 128
-// slots each): at step s lane l reads the sum of column s - l, subtracts its term and
-// writes it back, and one step later lane l + 1 reads what lane l wrote -- one wave's
-// DS instructions execute in issue order, and a compiler barrier between the steps
-// keeps their order in the code.  Before round 5 the sums travelled in registers one
-// lane per step (a DPP wave shift: 6 moves per step at D = 3) with a broadcast read
-// of the entering sum and a predicated store of the leaving one; here none of them.
-// The column's entering sum (from the sweeps before) is staged into its slot, and
-// its final sum is in the slot once lane 63 has passed it.
+// its running sum in LDS, in its slot of the column ring `col` (D components,
+// kColSlots slots each): at step s lane l reads the sum of column s - l, subtracts its
+// term and writes it back, and one step later lane l + 1 reads what lane l wrote --
+// one wave's DS instructions execute in issue order, and a compiler barrier between
+// the steps keeps their order in the code.  Before round 5 the sums travelled in
+// registers one lane per step (a DPP wave shift: 6 moves per step at D = 3) with a
+// broadcast read of the entering sum and a predicated store of the leaving one; here
+// none of them.  The column's entering sum (from the sweeps before) is staged into its
+// slot, and its final sum is in the slot once lane 63 has passed it.
+// During column tile tt the steps touch tiles tt - 1 and tt; they sit side by side,
+// tile tt - 1 at slots 0..63 and tile tt at 64..127, so lane l reads slot 64 - l + j at
+// step 64 tt + j, never wrapping: the current tile moves down to 0..63 (one LDS copy
+// per lane and component) before the next one is staged above it.  (Round 5 kept
+// column q at slot q & 127, which wrapped inside the even tiles: one select per step
+// there, 53-54 VALU per step against 50.  A 192-slot ring that moved only the even
+// tiles ran as fast but its 6 KB more LDS per block locked the resident classes'
+// kernels out of the CUs during the repulsion launch: attraction passes 4.48 against
+// 3.54 ms, profiles/r06/ab_colring.log.)
 // Records {x[D], deg+1} are component-major in the ring `rec` (D + 1 components,
 // kRecSlots slots each): column q at slot q & 127, and slots 0..63 mirrored at
 // 128..191, so that within a column tile every lane reads slot ((64 tt - l) & 127) + j
 // at step 64 tt + j without wrapping: the per-step addresses are immediate offsets.
-// The column ring wraps inside the even tiles only (tile tt holds slots
-// 64 (tt & 1) .. +63): there a lane switches base once.
-constexpr int kSymRing = 128;   // column ring (column q at q & 127)
+constexpr int kColSlots = 128;  // column ring: tile tt - 1 at 0..63, tile tt at 64..127
+constexpr int kSymRing = 128;   // record ring period (column q at q & 127)
 constexpr int kRecSlots = 192;  // record ring: 128 slots + the first 64 mirrored
+constexpr int kColBase = 64;    // the current tile's first slot
 
 // Compiler barrier between two steps: the next step's reads of the column ring
 // must stay after this step's writes (different slots for one lane, the same slot
-// for the next lane: a cross-lane dependency the compiler cannot see).
+// for the next lane: a cross-lane dependency the compiler cannot see).  Under the
+// HIP memory model this hand-off between lanes is a data race; it is correct because
+// one wave's DS instructions execute in issue order and the barrier keeps the issue
+// order.  A compiler that reordered DS operations across an asm memory clobber, or
+// hardware that completed them out of order, would change the bits: the canaries are
+// tests/test_gpu_parity.py::test_faml_symmetric_sweeps, ::test_fa_symmetric_repulsion*,
+// test_gpu_configs.py::test_c4_level0_oracle_at_embed_horizon (100 iterations at C4
+// against the oracle) and the 1e5-iteration coarsest fixture.
 __device__ __forceinline__ void step_barrier() { asm volatile("" ::: "memory"); }
 
 // One step of a sweep at any position (runtime step index sg): the diagonal tiles
 // (DIAG: a lane takes its own row's sum over from the column that reaches it), the
 // drain, and tiles outside the shared-reciprocal domain (SHARED = false).
+// coff: kColBase - 64 tt of the step's tile (column q at slot coff + q).
 template <int D, bool SHARED, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void col_step(int sg, int lane, const double* rec, double* col,
+__device__ __forceinline__ void col_step(int sg, int lane, int coff, const double* rec, double* col,
                                          const double (&xr)[D], double dr, double repel,
                                          double (&racc)[D]) {
   const int q = sg - lane;
   const int p = q & (kSymRing - 1);
+  const int pc = coff + q;
   double xq[D + 1], c[D];
 #pragma unroll
   for (int k = 0; k <= D; ++k) xq[k] = rec[k * kRecSlots + p];
 #pragma unroll
-  for (int k = 0; k < D; ++k) c[k] = col[k * kSymRing + p];
+  for (int k = 0; k < D; ++k) c[k] = col[k * kColSlots + pc];
   if (DIAG && q == lane) {  // column q = this lane's row: its sum so far is the row's
 #pragma unroll
     for (int k = 0; k < D; ++k) racc[k] = c[k];
@@ -110,67 +128,56 @@ __device__ __forceinline__ void col_step(int sg, int lane, const double* rec, do
 #pragma unroll
   for (int k = 0; k < D; ++k) {
     racc[k] = racc[k] + t[k];
-    col[k * kSymRing + p] = c[k] - t[k];
+    col[k * kColSlots + pc] = c[k] - t[k];
   }
   step_barrier();
 }
 
 template <int D, bool REPEL_ONE, bool DIAG>
-__device__ __forceinline__ void col_steps(bool fast, int s0, int s1, int lane, const double* rec,
-                                          double* col, const double (&xr)[D], double dr,
-                                          double repel, double (&racc)[D]) {
+__device__ __forceinline__ void col_steps(bool fast, int s0, int s1, int lane, int coff,
+                                          const double* rec, double* col, const double (&xr)[D],
+                                          double dr, double repel, double (&racc)[D]) {
   if (fast)
     for (int sg = s0; sg < s1; ++sg)
-      col_step<D, true, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc);
+      col_step<D, true, REPEL_ONE, DIAG>(sg, lane, coff, rec, col, xr, dr, repel, racc);
   else
     for (int sg = s0; sg < s1; ++sg)
-      col_step<D, false, REPEL_ONE, DIAG>(sg, lane, rec, col, xr, dr, repel, racc);
+      col_step<D, false, REPEL_ONE, DIAG>(sg, lane, coff, rec, col, xr, dr, repel, racc);
 }
 
 // The 64 steps of a full column tile tt >= 2 in the shared-reciprocal domain (the
 // bulk of every sweep): eight blocks of eight steps, every LDS access an immediate
-// offset from a per-block base.  EVEN: tt even, where lanes l > j read slot
-// 128 + j - l and lanes l <= j slot j - l (one select per step).  No prefetch of the
-// next step's records into a second register set: the other waves of the SIMD hide
-// the LDS latency, and the kernel must stay within 120 VGPRs (see faml_sym_repulse).
-template <int D, bool REPEL_ONE, bool EVEN>
+// offset from a per-block base, the same code in odd and even tiles.  No prefetch of
+// the next step's records into a second register set: the other waves of the SIMD
+// hide the LDS latency, and the kernel must stay within 120 VGPRs (see
+// faml_sym_repulse).
+template <int D, bool REPEL_ONE>
 __device__ __forceinline__ void tile_steps(int tt, int lane, const double* rec, double* col,
                                            const double (&xr)[D], double dr, double repel,
                                            double (&racc)[D]) {
   const double* rb = rec + ((64 * tt - lane) & (kSymRing - 1));
-  double* cb = col + (EVEN ? kSymRing - lane : 64 - lane);
+  double* cb = col + kColBase - lane;
   for (int j0 = 0; j0 < 64; j0 += 8) {
     const double* rj = rb + j0;
     double* cj = cb + j0;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       double* cp = cj + jj;
-      if (EVEN && j0 + jj >= lane) cp -= kSymRing;
       double c[D], xq[D + 1];
 #pragma unroll
       for (int k = 0; k <= D; ++k) xq[k] = rj[k * kRecSlots + jj];
 #pragma unroll
-      for (int k = 0; k < D; ++k) c[k] = cp[k * kSymRing];
+      for (int k = 0; k < D; ++k) c[k] = cp[k * kColSlots];
       double t[D];
       rep_term<D, true, REPEL_ONE>(xr, xq, dr, xq[D], repel, t);
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         racc[k] = racc[k] + t[k];
-        cp[k * kSymRing] = c[k] - t[k];
+        cp[k * kColSlots] = c[k] - t[k];
       }
       step_barrier();
     }
   }
-}
-
-template <int D, bool REPEL_ONE>
-__device__ __forceinline__ void tile_steps_any(int tt, int lane, const double* rec, double* col,
-                                               const double (&xr)[D], double dr, double repel,
-                                               double (&racc)[D]) {
-  if (tt & 1)
-    tile_steps<D, REPEL_ONE, false>(tt, lane, rec, col, xr, dr, repel, racc);
-  else
-    tile_steps<D, REPEL_ONE, true>(tt, lane, rec, col, xr, dr, repel, racc);
 }
 
 // Hand-over slot of member c, dimension k: component-major H[k * hs + c].
@@ -184,16 +191,18 @@ __device__ __forceinline__ double* hand_at(double* H, size_t hs, size_t c, int k
 // The hand-over buffer H is component-major (H[k * hs + c]): each of the D store
 // instructions covers 512 contiguous bytes (8 lines) instead of the 24 lines a
 // 24-byte-strided record store spans, which the agent-scope stores pay per line.
+// `at`: the column ring slot of the tile's first column (0: it has moved down, the
+// tile after it is current).
 template <int D>
 __device__ __forceinline__ void sym_handover(int t, int lane, int done, int ncols, size_t cbase,
-                                             const double* col, double* H, size_t hs,
+                                             const double* col, int at, double* H, size_t hs,
                                              int* tprog) {
   wave_lds_sync();
   const int qo = 64 * t + lane;
   if (qo < ncols) {
-    const double* o = col + (qo & (kSymRing - 1));
+    const double* o = col + at + lane;
 #pragma unroll
-    for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, cbase + qo, k), o[k * kSymRing]);
+    for (int k = 0; k < D; ++k) agent_st(hand_at<D>(H, hs, cbase + qo, k), o[k * kColSlots]);
   }
   // Ordering (no acquire/release: an agent-scope release would write back the whole
   // L2, ~every 64 steps): the sums are agent-scope stores (they bypass the per-XCD
@@ -377,10 +386,15 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     if (cv) dc = DP[cbase + qc];
     const bool ok_cur = __all(!cv || vertex_ok<D>(xc, dc));
     const int p = qc & (kSymRing - 1);
+    if (tt > 0) {  // the tile before moves down to 0..63 (its hand-over has read 0..63)
+#pragma unroll
+      for (int k = 0; k < D; ++k) col[k * kColSlots + lane] = col[k * kColSlots + kColBase + lane];
+    }
+    const int cb = kColBase;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       rec[k * kRecSlots + p] = xc[k];
-      col[k * kSymRing + p] = ic[k];  // the column enters with its sum so far
+      col[k * kColSlots + cb + lane] = ic[k];  // the column enters with its sum so far
     }
     rec[D * kRecSlots + p] = dc;
     if (!(tt & 1)) {  // slots 0..63 are mirrored at 128..191
@@ -391,16 +405,17 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
     wave_lds_sync();
     // the steps of tile tt read tiles tt-1 and tt; the diagonal meets steps < 127
     const bool fast = rows_ok && ok_cur && ok_prev;
+    const int coff = cb - 64 * tt;
     if (tt < 2)
-      col_steps<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
-                                    racc);
+      col_steps<D, REPEL_ONE, true>(fast, 64 * tt, 64 * tt + 64, lane, coff, rec, col, xr, dr,
+                                    repel, racc);
     else if (fast)
-      tile_steps_any<D, REPEL_ONE>(tt, lane, rec, col, xr, dr, repel, racc);
+      tile_steps<D, REPEL_ONE>(tt, lane, rec, col, xr, dr, repel, racc);
     else
-      col_steps<D, REPEL_ONE, false>(false, 64 * tt, 64 * tt + 64, lane, rec, col, xr, dr, repel,
-                                     racc);
+      col_steps<D, REPEL_ONE, false>(false, 64 * tt, 64 * tt + 64, lane, coff, rec, col, xr, dr,
+                                     repel, racc);
     ok_prev = ok_cur;
-    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, col, H, hs, tprog);
+    if (tt >= 2) sym_handover<D>(tt - 1, lane, A + 1, ncols, cbase, col, cb - 64, H, hs, tprog);
     wave_lds_sync();  // the slots of tile tt-1 are free for tile tt+1
   }
   {  // drain: the last columns cross the wave; the slots past them hold inert records
@@ -410,15 +425,21 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
       rec[k * kRecSlots + p] = 0.0;
       if (!(ntiles & 1)) rec[k * kRecSlots + p + kSymRing] = 0.0;
     }
+    // the drain is tile ntiles: the last tile moves down to 0..63
+#pragma unroll
+    for (int k = 0; k < D; ++k) col[k * kColSlots + lane] = col[k * kColSlots + kColBase + lane];
     wave_lds_sync();
   }
   const int s0 = 64 * ntiles, s1 = ncols + 63;
+  const int cbd = kColBase, coff = cbd - 64 * ntiles;
   if (ntiles < 2)
-    col_steps<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel, racc);
+    col_steps<D, REPEL_ONE, true>(rows_ok && ok_prev, s0, s1, lane, coff, rec, col, xr, dr, repel,
+                                  racc);
   else
-    col_steps<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, rec, col, xr, dr, repel,
+    col_steps<D, REPEL_ONE, false>(rows_ok && ok_prev, s0, s1, lane, coff, rec, col, xr, dr, repel,
                                    racc);
-  if (ntiles >= 2) sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, col, H, hs, tprog);
+  if (ntiles >= 2)
+    sym_handover<D>(ntiles - 1, lane, A + 1, ncols, cbase, col, cbd - 64, H, hs, tprog);
   // the rows' sums: the caller writes them to F
 #pragma unroll
   for (int k = 0; k < D; ++k) rout[k] = racc[k];
@@ -468,7 +489,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
   // doubles) and the column ring
   static_assert(kRecSlots * (D + 1) >= 64 * SymW<D>::v, "row-block tile fits the record ring");
   __shared__ __attribute__((aligned(16))) double srec[NW][kRecSlots * (D + 1)];
-  __shared__ __attribute__((aligned(16))) double scol[NW][kSymRing * D];
+  __shared__ __attribute__((aligned(16))) double scol[NW][kColSlots * D];
   const int lane = threadIdx.x & 63;
   double* rec = srec[threadIdx.x >> 6];
   double* col = scol[threadIdx.x >> 6];

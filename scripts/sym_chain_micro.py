@@ -2,7 +2,8 @@
 tiles) alone on the GPU, every row tile a symmetric sweep (GE_FAML_SYM_CHAIN=0), so
 the launch is a single convoy of T sweeps.  Prints per s the repulsion launch time
 and the lag per sweep (launch / T) -- the tile-time of a chain with the rest of the
-GPU idle.  Compare GE_SYM_FLOW=0 / 1.
+GPU idle (round 6: 43 us per sweep at T = 656, profiles/r06/chain_micro_ring.log; the
+register-flow variant measured against it is described in DESIGN.md 5d).
 
 usage: python scripts/sym_chain_micro.py [s ...]     (default 4096 16384 41984)
 """
@@ -45,8 +46,7 @@ def main():
         ctx.sync()
         ms = p.repulse_ms()[0]
         tiles = (s + 63) // 64
-        print(json.dumps({"s": s, "tiles": tiles, "flow": os.environ.get("GE_SYM_FLOW", ""),
-                          "schedule": p.schedule(), "repulse_ms": ms,
+        print(json.dumps({"s": s, "tiles": tiles, "schedule": p.schedule(), "repulse_ms": ms,
                           "us_per_sweep": ms * 1e3 / tiles,
                           "us_per_step_on_chain": ms * 1e3 / (3 * s)}), flush=True)
         p.close()

@@ -21,8 +21,10 @@ def rel_err(x, ref):
 # exact arithmetic building blocks
 
 def test_shared_reciprocal_division_is_ieee(ctx):
-    # 3 checks per sample; 2^26 samples ~ 2e8 divisions compared bitwise to `/`
-    assert ctx.selftest_math(1 << 26, seed=7) == 0
+    # 2^30 draws (those whose operands lie in the exact-division domain -- most of
+    # them -- are compared): every repulsion term of pair_den against the rcp-based
+    # reciprocals and against `/`, bitwise (ge_selftest.hip, ge_pair.hpp pair_den)
+    assert ctx.selftest_math(1 << 30, seed=7) == 0
 
 
 # --------------------------------------------------------------------------
