@@ -841,14 +841,9 @@ __device__ __forceinline__ bool stage_records(const double* __restrict__ X,
 // the acquire invalidate each cost more than the whole barrier's ordering is worth
 // here, so the shipped order is 0: agent-scope (L2-bypassing) stores and loads of
 // the coordinates, every store completed (s_waitcnt 0) before the arrival.
-// GE_DIAG_COARSE (diagnostics variants, scripts/build_variant.sh; wrong results): 1
-// packed rows skip their chunks, 2 also the staging -- what is left is the barrier,
-// the staging and the row update; 5 (right results) thread 0 of blocks 0, nb/2 and
-// nb-1 prints its microseconds per iteration in each phase at the end of the launch;
-// 6 (right results) as 5, with the adder's cycles of its adds alone.
-#ifndef GE_DIAG_COARSE
-#define GE_DIAG_COARSE 0
-#endif
+// (Round 5 measured the phases of an iteration with diagnostics builds of this
+// kernel -- per-phase clock stamps, chunks or staging skipped -- DESIGN.md 5c,
+// profiles/r05/coarsest_phase_diag.log; removed from the source in round 6.)
 #ifndef GE_BAR_ORDER
 #define GE_BAR_ORDER 0
 #endif
@@ -1092,10 +1087,8 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
                                                  const double* __restrict__ X,
                                                  const double* __restrict__ dp1, const FaConst& c,
                                                  double* __restrict__ Fprev,
-                                                 double* __restrict__ Xnext, double* smem,
-                                                 long long* dt = nullptr) {
+                                                 double* __restrict__ Xnext, double* smem) {
   static_assert(R * D <= 64, "one adder lane per (row, dimension)");
-  const long long tp0 = (GE_DIAG_COARSE >= 5 && dt) ? wall_clock64() : 0;
   static_assert(kPackC % 16 == 0 && kPackS % 2 == 0, "chain_prefetch reads 16-byte pairs");
   constexpr int W = Rec<D>::W;
   constexpr int PL = kGrpT - 64;               // producer lanes
@@ -1108,13 +1101,9 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
   double* tb = smem + (size_t)n * W;
   const int tid = threadIdx.x;
   const int r0 = rb + blk * R;
-#if GE_DIAG_COARSE == 2  // diagnostics variant (wrong results): no staging
-  const bool ok = true;
-#else
   const bool ok =
       stage_records<D, kGrpT, 4, COH && kBarCohStage>(X, dp1, 0, n, rec) &&
       (REPEL_ONE || weight_ok(c.repel));
-#endif
   if (tid < R) {
     const int i = r0 + tid;
     s_e[tid][0] = i < re ? ip[i] : 0;
@@ -1178,66 +1167,27 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
 #pragma unroll
   for (int r = 0; r < R; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
   const int natt = (maxdeg + kPackC - 1) / kPackC;
-#if GE_DIAG_COARSE == 1 || GE_DIAG_COARSE == 2  // diagnostics (wrong results): no terms
-  const int ntot = 0;
-#else
   const int ntot = nrep + natt;  // the repulsion chunks, then the attraction chunks
-#endif
   const int adeg = adder ? s_e[ar][1] - s_e[ar][0] : 0;
-  const long long tp1 = (GE_DIAG_COARSE >= 5 && dt) ? wall_clock64() : 0;
   if (prod && ntot > 0) {
     if (nrep > 0) rep_chunk(0, tb);
     else att_chunk(0, tb);
   }
   __syncthreads();
-  long long busy = 0, busy_adds = 0;  // GE_DIAG_COARSE 5 / 6: clock64 cycles in the loop
-#ifdef GE_DIAG_ADDER_PRIO  // diagnostics variant: the adder wave at issue priority 3
-  if (tid < 64) __builtin_amdgcn_s_setprio(3);
-#endif
   for (int ch = 0; ch < ntot; ++ch) {
     const double* cur = tb + (ch & 1) * BUF;
-    const long long tc0 = GE_DIAG_COARSE >= 5 ? clock64() : 0;
     if (tid < 64) {
       if (adder) {
         const int cnt = ch < nrep ? min(kPackC, n - ch * kPackC)
                                   : min(kPackC, max(0, adeg - (ch - nrep) * kPackC));
-#if GE_DIAG_COARSE == 6  // diagnostics: every term in registers first, then the adds timed
-        if (cnt > 0) {
-          double v[kPackC];
-          const double* q = cur + (ar * D + ak) * kPackS;
-#pragma unroll
-          for (int l = 0; l < kPackC; ++l) v[l] = (l < cnt) ? q[l] : 0.0;
-          __builtin_amdgcn_s_waitcnt(0);
-          const long long ta = clock64();
-#pragma unroll
-          for (int l = 0; l < kPackC; ++l) a = a + v[l];
-          __asm__ volatile("" : "+v"(a));
-          busy_adds += clock64() - ta;
-        }
-#else
         if (cnt > 0) a = chain_prefetch<kPackC>(a, cur + (ar * D + ak) * kPackS, cnt);
-#endif
       }
     } else if (ch + 1 < ntot) {
       double* nxt = tb + ((ch + 1) & 1) * BUF;
       if (ch + 1 < nrep) rep_chunk(ch + 1, nxt);
       else att_chunk(ch + 1 - nrep, nxt);
     }
-    if (GE_DIAG_COARSE >= 5) {
-      __builtin_amdgcn_s_waitcnt(0);
-      busy += clock64() - tc0;
-    }
     __syncthreads();
-  }
-#ifdef GE_DIAG_ADDER_PRIO
-  if (tid < 64) __builtin_amdgcn_s_setprio(0);
-#endif
-  if (GE_DIAG_COARSE >= 5 && dt && (tid == 0 || tid == 64))
-    dt[tid == 0 ? 4 : 5] += (GE_DIAG_COARSE == 6 && tid == 0 ? busy_adds : busy) / max(ntot, 1);
-  if (GE_DIAG_COARSE >= 5 && dt && tid == 0) {
-    const long long tp2 = wall_clock64();
-    dt[0] += tp1 - tp0;  // staging
-    dt[1] += tp2 - tp1;  // chunks
   }
   if (tid < 64) {
     // the row's leader lane (r * D) gathers its dimensions, then gravity / update
@@ -1347,16 +1297,12 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
                       long long limit) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_ok;
-  long long dt[6] = {0, 0, 0, 0, 0, 0};  // GE_DIAG_COARSE 5: staging, chunks, rest, barrier,
-                                         // adder / producer cycles per chunk
-  long long tb0 = 0;
   for (int it = 0; it < iterations; ++it) {
     const double* X = (it & 1) ? Xb : Xa;
     double* Xn = (it & 1) ? Xa : Xb;
-    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) tb0 = wall_clock64();
     if constexpr (PACKED > 0)
       packed_iteration<D, REPEL_ONE, LINEAR, true, PACKED>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1, c,
-                                                   Fprev, Xn, smem, dt);
+                                                   Fprev, Xn, smem);
     else
       grouped_iteration<D, G, REPEL_ONE, LINEAR, true>(blockIdx.x, n, 0, n, ip, ix, dx, X, dp1,
                                                        c, Fprev, Xn, smem);
@@ -1367,29 +1313,11 @@ fa_grouped_persistent(int n, const int* __restrict__ ip, const int* __restrict__
     __builtin_amdgcn_s_waitcnt(0);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __syncthreads();
-    long long tw = 0;
-    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) tw = wall_clock64();
     if (threadIdx.x == 0) s_ok = grid_arrive_wait(bar, gridDim.x, it, limit) ? 1 : 0;
     __syncthreads();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0) {
-      const long long te = wall_clock64();
-      dt[2] += tw - tb0 - 0;  // the whole iteration before the barrier (minus the phases below)
-      dt[3] += te - tw;
-    }
     if (!s_ok) return;
   }
-  if (GE_DIAG_COARSE >= 5 && threadIdx.x == 0 &&
-      (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1)) {
-    const double us = 0.01 / (iterations > 1 ? iterations - 1 : 1);  // 100 MHz ticks
-    printf("coarse diag block %d: staging %.2f chunks %.2f rest %.2f barrier %.2f us/iteration;"
-           " adder %lld cycles per chunk; HW_ID %x\n",
-           (int)blockIdx.x, dt[0] * us, dt[1] * us, (dt[2] - dt[0] - dt[1]) * us, dt[3] * us,
-           dt[4] / iterations, __builtin_amdgcn_s_getreg((31 << 11) | 4));
-  }
-  if (GE_DIAG_COARSE >= 5 && threadIdx.x == 64 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
-    printf("coarse diag block %d: producer wave %lld cycles per chunk; HW_ID %x\n", (int)blockIdx.x,
-           dt[5] / iterations, __builtin_amdgcn_s_getreg((31 << 11) | 4));
 }
 
 // Mid-size levels (grouped_cap < n <= kStreamMax): the same fused iteration
@@ -1765,8 +1693,6 @@ static void sym_prepare(ge_fa_plan* pl) {
     pl->seg.upload(h_seg, 2, s);
     pl->hand.alloc((size_t)pl->n * pl->dim);
     pl->sym_blocks = pl->cus * sym_blocks_per_cu(pl->dim);
-    if (const char* e = std::getenv("GE_FA_SYM_BLOCKS"))  // tuning: blocks per CU
-      pl->sym_blocks = pl->cus * std::max(1, std::min(4, std::atoi(e)));
     int dev = 0, khz = 0;
     GE_HIP(hipGetDevice(&dev));
     GE_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
@@ -1900,9 +1826,6 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
       const int nbk = pk ? (n + R - 1) / R : nb;
       size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D, R))
                       : grouped_lds_bytes(n, D);
-#ifdef GE_DIAG_LDS_MIN  // diagnostics variant: LDS per block raised (fewer blocks per CU)
-      lds = std::max(lds, (size_t)GE_DIAG_LDS_MIN);
-#endif
       const void* fn =
           !pk    ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>)
           : R == 6 ? reinterpret_cast<const void*>(

@@ -923,9 +923,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // three blocks (waves) per SIMD of the four that fit: fewer units in flight spin
     // less on hand-overs (C4 N = 1: 137.2 against 138.3 ms per launch; N = 8 shares
     // 30.0 against 32.7 ms; scripts/sym_timeline.py, profiles/r03/sym_timeline)
-    int bpc = std::min(std::max(occ, 1), 3);
-    if (const char* e = std::getenv("GE_FAML_SYM_BLOCKS"))  // tuning override
-      bpc = std::max(1, std::min(std::max(occ, 1), std::atoi(e)));
+    const int bpc = std::min(std::max(occ, 1), 3);
     pl->sym_blocks = cus * bpc;
     const double waves = (double)pl->sym_blocks * (kSymT / 64);
     // Per streamed aggregate: symmetric sweeps or whole row blocks.  The launch lasts
@@ -945,9 +943,9 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // unordered), wave time at full load -- 0.6 measured on an N = 8 share of C4
     // (all row blocks: 17.9 us per row tile per wave, against 29.8 us per sweep tile
     // at N = 1; profiles/r04/sym_timeline_rows_n8.json)
-    double chain_k = 2.5, row_k = 0.6;
+    double chain_k = 2.5;
+    const double row_k = 0.6;
     if (const char* e = std::getenv("GE_FAML_SYM_CHAIN")) chain_k = std::atof(e);  // 0: all sweeps
-    if (const char* e = std::getenv("GE_FAML_SYM_ROWK")) row_k = std::atof(e);
     std::vector<char> as_rows(big.size(), 0);
     double best = 0.0;
     if (chain_k > 0.0 && any_big) {
@@ -977,14 +975,6 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
       for (size_t k = 0; k < best_k; ++k) as_rows[by_T[k]] = 1;
       best = pbest;
     }
-    if (std::getenv("GE_FAML_PLAN_DEBUG") && any_big) {
-      int nr = 0;
-      for (size_t b = 0; b < big.size(); ++b) nr += as_rows[b];
-      std::fprintf(stderr,
-                   "faml plan: %zu streamed aggregates, T max %d, waves %.0f, %d as row blocks, "
-                   "predicted %.1f tile-times\n",
-                   big.size(), *std::max_element(T.begin(), T.end()), waves, nr, best);
-    }
     pl->rows_mode = pl->swept = 0;
     for (size_t b = 0; b < big.size(); ++b) {
       if (as_rows[b]) ++pl->rows_mode;
@@ -997,34 +987,30 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
     // every aggregate's sweeps spread over the whole queue, so all aggregates reach
     // their last (chain-bound) sweeps together and the launch ends without a tail of
     // the largest aggregate's chain (C4: tail after the queue drained 8.7 -> 3.5 ms,
-    // 148.1 -> 143.2 ms per launch).  GE_FAML_SYM_PROP=0: 2A, the sweep's earliest
-    // start (diagnostics; GE_FAML_SYM_EST scales the 2).  Every sweep comes after the
-    // sweeps it waits on (sweep A - 1 before A).
-    double est_k = 2.0;
-    if (const char* e = std::getenv("GE_FAML_SYM_EST")) est_k = std::atof(e);
-    const bool est_prop = !(std::getenv("GE_FAML_SYM_PROP") && *std::getenv("GE_FAML_SYM_PROP") == '0');
+    // 148.1 -> 143.2 ms per launch; 2A alone, the sweep's earliest start, was the
+    // round-2 order).  Every sweep comes after the sweeps it waits on (sweep A - 1
+    // before A).
+    const double est_k = 2.0;
     const int Tmax = big.empty() ? 1 : *std::max_element(T.begin(), T.end());
     // Big aggregates a little ahead: positions also scaled by 1 - g T / Tmax (g = 0.3),
     // so the largest chains finish before the queue's end and the small aggregates'
     // short chains fill it (C4, one box, 3 rounds interleaved: 136.2-136.4 against
     // 136.9-137.3 ms per step; g = 0.15 136.5-136.7, 0.5 and 0.7 slower;
     // profiles/r04/ab_big_first.log).  Positions stay increasing in A for g < 1, so
-    // every unit still waits only on units before it.  GE_FAML_SYM_BIGFIRST=g overrides.
-    double big_first = 0.3;
-    if (const char* e = std::getenv("GE_FAML_SYM_BIGFIRST"))
-      big_first = std::min(0.9, std::max(0.0, std::atof(e)));
+    // every unit still waits only on units before it.
+    const double big_first = 0.3;
     auto scale_of = [&](int Tb) {
-      return (est_prop ? (double)Tmax / Tb : 1.0) * (1.0 - big_first * Tb / Tmax);
+      return ((double)Tmax / Tb) * (1.0 - big_first * Tb / Tmax);
     };
     // row blocks' issue priority: one level per quarter of the longest row block's
-    // column tiles (ge_sym.hpp rows_prio; GE_FAML_ROWS_PRIO=0: all at priority 3)
-    // (GE_FAML_ROWS_PRIO=k: one level per 1/k of it instead, tuning)
-    int rows_q = 0, prio_div = 4;
-    if (const char* e = std::getenv("GE_FAML_ROWS_PRIO")) prio_div = std::atoi(e);
+    // column tiles (ge_sym.hpp rows_prio; one level per sixth or eighth: no different,
+    // profiles/r05/scale_sim_c4_prio_divisor.log)
+    int rows_q = 0;
+    const int prio_div = 4;
     for (size_t b = 0; b < big.size(); ++b)
       if (as_rows[b]) rows_q = std::max(rows_q, T[b]);
     for (int a : split) rows_q = std::max(rows_q, (h_pt_ip[a + 1] - h_pt_ip[a] + 63) / 64);
-    rows_q = prio_div > 0 ? (rows_q + prio_div - 1) / prio_div : 0;
+    rows_q = (rows_q + prio_div - 1) / prio_div;
     for (size_t b = 0; b < big.size(); ++b) {
       if (as_rows[b]) {
         // row blocks have no dependencies and each spans its aggregate's whole width:
@@ -1088,9 +1074,7 @@ static void faml_plan_build(ge_faml_plan* pl, const int* h_pt_ip, const std::vec
   // 4 waves per SIMD: more items per wave for the queue to balance (C3 level
   // 0: 961 ms per call against 1091 ms at the full 8 waves per SIMD)
   const int occ = rep_occupancy(dim, pl->code);
-  int blocks_cu = std::min(4, occ);
-  if (const char* e = std::getenv("GE_FAML_BLOCKS_PER_CU"))  // tuning override
-    blocks_cu = std::max(1, std::min(occ, std::atoi(e)));
+  const int blocks_cu = std::min(4, occ);
   pl->rep_blocks = cus * blocks_cu;
   std::vector<int> begs;
   begs.insert(begs.end(), beg_s.begin(), beg_s.end());
@@ -1232,20 +1216,8 @@ static void faml_plan_run(ge_faml_plan* pl, const double* cA, const double* rA, 
           const size_t hs = (size_t)pl->n;
           int* err = pl->sym_err.p;
           const long long lim = pl->sym_limit;
-          if (false) {
-#ifdef GE_SYM_DIAGNOSTICS
-          } else if (!pl->stamp_path.empty() && std::getenv("GE_SYM_NOWAIT")) {
-            // timing only, WRONG results: no sweep waits for its hand-overs.  Built
-            // only with -DGE_SYM_DIAGNOSTICS (scripts/build_variant.sh NAME -DGE_SYM_DIAGNOSTICS), never in the
-            // shipped library.
-            std::fprintf(stderr, "libge: GE_SYM_NOWAIT diagnostics build: results are invalid\n");
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, true>), dim3(pl->sym_blocks),
-                               dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
-                               pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
-                               err, lim, pl->stamps.p);
-#endif
-          } else if (!pl->stamp_path.empty()) {
-            hipLaunchKernelGGL((faml_sym_repulse<D, false, true, false>), dim3(pl->sym_blocks),
+          if (!pl->stamp_path.empty()) {
+            hipLaunchKernelGGL((faml_sym_repulse<D, false, true>), dim3(pl->sym_blocks),
                                dim3(kSymT), 0, ss, pl->nunits, pl->units.p, pl->queue.p + it,
                                pl->pt_ip, cur, pl->DP.p, c.repel, pl->Fscr.p, H, hs, pl->prog.p,
                                err, lim, pl->stamps.p);

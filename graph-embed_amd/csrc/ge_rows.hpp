@@ -59,7 +59,6 @@ struct RowClasses {
   const int* seg = nullptr;       // nseg x {heavy row slot, first, last entry offset in the row}
   long long* hacc = nullptr;      // nheavy x D x {S, A}: binade sums of the segments (zeroed)
   int* hflag = nullptr;           // nheavy: a segment could not use the binade sum
-  int* nfall = nullptr;           // count of heavy-row passes summed serially (GE_ROWS_STATS)
   double* hterm = nullptr;        // kSegStore: the heavy rows' terms, row h at hoff[h], dim-major
   const long long* hoff = nullptr;
   int seg_mode = 0;               // kSegBinade / kSegStore when nseg > 0
@@ -532,7 +531,6 @@ __global__ void __launch_bounds__(kRowT) heavy_finish_kernel(RowClasses L, P p) 
 #pragma unroll
     for (int k = 0; k < D; ++k) st.acc[k] = sum[k];
   } else {
-    if (lane == 0 && L.nfall) atomicAdd(L.nfall, 1);
     ordered_edge_sum<D, 1>(st.e0, st.e1, lane, buf + (tid >> 6) * 64 * D,
                            [&](int e, double (&t)[D]) { p.term(st, e, t); }, st.acc);
   }
@@ -684,7 +682,7 @@ __global__ void __launch_bounds__(kRowT, GE_ROWS_MINBLOCKS) classed_rows_kernel(
 // beside the tiles, and the heavy rows' binade accumulators (segment mode).
 struct RowStreams {
   DevBuf<long long> hacc, hoff;
-  DevBuf<int> hflag, nfall;
+  DevBuf<int> hflag;
   DevBuf<double> hterm;
   int nheavy = 0;
   // allocate (and zero) the heavy rows' segment buffers; deg: their entry
@@ -709,11 +707,6 @@ struct RowStreams {
     rc.hacc = hacc.p;
     rc.hflag = hflag.p;
     nheavy = rc.nheavy;
-    if (std::getenv("GE_ROWS_STATS")) {
-      nfall.alloc(1);
-      GE_HIP(hipMemsetAsync(nfall.p, 0, sizeof(int), s));
-      rc.nfall = nfall.p;
-    }
   }
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
@@ -721,11 +714,6 @@ struct RowStreams {
   RowStreams(const RowStreams&) = delete;
   RowStreams& operator=(const RowStreams&) = delete;
   ~RowStreams() {
-    if (nfall.p) {
-      int v = 0;
-      if (hipMemcpy(&v, nfall.p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess)
-        std::fprintf(stderr, "rows: %d heavy rows, %d serial fallbacks in total\n", nheavy, v);
-    }
     if (side) {
       (void)hipStreamSynchronize(side);
       (void)hipStreamDestroy(side);

@@ -341,7 +341,7 @@ constexpr int kStampWords = 8;
 // One symmetric sweep (unit kind 0): row tile A against the columns >= 64A, the
 // column sums handed to the next sweep tile by tile.  rec / col: this wave's rings
 // (see kSymRing).  STAMP: spin ticks and the first hand-over time.
-template <int D, bool REPEL_ONE, bool STAMP, bool NOWAIT = false>
+template <int D, bool REPEL_ONE, bool STAMP>
 __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int* tprog,
                                            const double* __restrict__ X,
                                            const double* __restrict__ DP, double repel,
@@ -364,7 +364,7 @@ __device__ __forceinline__ void sweep_unit(int lane, int A, int base, int s, int
   const int ntiles = (ncols + 63) >> 6;
   bool ok_prev = true;
   for (int tt = 0; tt < ntiles; ++tt) {
-    if (A > 0 && !NOWAIT) {  // the sweeps 0..A-1 have written column tile A + tt back
+    if (A > 0) {  // the sweeps 0..A-1 have written column tile A + tt back
       const long long w = handover_wait<STAMP>(tprog + tt, A, err, limit, give_up);
       if (STAMP) {
         spin += w;
@@ -468,8 +468,9 @@ constexpr int kUnitSweep = 0, kUnitRows = 1;
 // block: its priority quantum), kind}
 // in queue order; prog (ptiles progress counters) zeroed before the launch; queue =
 // one counter.  Every unit waits only on units before it in the queue.
-// 4 waves per SIMD: <= 128 VGPRs, 40 KB of LDS per block (D = 3).  NOWAIT
-// (diagnostics, wrong results): no sweep waits for its hand-overs.
+// 4 waves per SIMD: <= 128 VGPRs, 36 KB of LDS per block (D = 3).  (Round 3 timed a
+// diagnostics build in which no sweep waited for its hand-overs -- wrong results --
+// at 124 against 138 ms; removed from the source in round 6.)
 // The kernel stays at <= 120 VGPRs: three of its waves per SIMD (the plan's three
 // blocks per CU) then leave 152 of the 512 registers, room for one wave of the
 // resident classes' kernels (143 VGPRs) on the other streams.  At 122-128 (with the
@@ -477,7 +478,7 @@ constexpr int kUnitSweep = 0, kUnitRows = 1;
 // resident kernels were locked out until the repulsion launches ended and ran
 // during the attraction passes instead (C4: 4.44 against 3.52 ms per pass, 140.4
 // against 137.0-137.3 ms per step; profiles/r04/ab_rows_r03.log).
-template <int D, bool REPEL_ONE, bool STAMP = false, bool NOWAIT = false>
+template <int D, bool REPEL_ONE, bool STAMP = false>
 __global__ void __launch_bounds__(kSymT, 4)
 faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ queue,
                  const int* __restrict__ pt_ip, const double* __restrict__ X,
@@ -514,7 +515,7 @@ faml_sym_repulse(int nunits, const int4* __restrict__ units, int* __restrict__ q
       rows_block<D, REPEL_ONE>(lane, base, s, A, X, DP, repel, repel_ok, rec, F, u.z);
     } else {  // a sweep
       double racc[D];
-      sweep_unit<D, REPEL_ONE, STAMP, NOWAIT>(lane, A, base, s, prog + u.z + A, X, DP, repel,
+      sweep_unit<D, REPEL_ONE, STAMP>(lane, A, base, s, prog + u.z + A, X, DP, repel,
                                               repel_ok, F, H, hs, err, limit, give_up, rec, col,
                                               spin, t_first, racc);
       if (64 * A + lane < s) {

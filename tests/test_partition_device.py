@@ -63,6 +63,17 @@ def test_partition_device_rmat(ctx, oracle, n, draws, cf):
     same(ctx.partition(A, cf), oracle.partition(A, cf))
 
 
+@pytest.mark.parametrize("mode", ["GE_PARTITION_NO_PATCH", "GE_PARTITION_FULL_SCANS"])
+def test_partition_device_alternative_paths(ctx, oracle, monkeypatch, mode):
+    """The device partition's two exact shortcuts switched off one at a time: every
+    dirty list rebuilt instead of hub lists patched in place, and every untouched
+    vertex rescanned in every pass instead of the recorded-bound skips (DESIGN.md 5,
+    partition rounds).  Same hierarchy as the oracle either way."""
+    monkeypatch.setenv(mode, "1")
+    A = G.largest_component(G.rmat(30000, 240000, seed=17))
+    same(ctx.partition(A, 0.125), oracle.partition(A, 0.125))
+
+
 def test_partition_device_er_and_components(ctx, oracle):
     # several components (no LCC) and an ER graph: ties everywhere
     A = G.rmat(3000, 6000, seed=11)
