@@ -520,7 +520,16 @@ def run_multilevel(args, rank, world, local, dev):
                                 "algorithmic_bytes_per_launch": att_bytes,
                                 "bytes_per_unit": "12 per CSR entry + 52 per row (SURVEY.md 8(d))",
                                 "rows": att_rows, "entries": att_entries,
-                                "avg_launch_ms": att_ms, "launches": att_passes},
+                                "avg_launch_ms": att_ms, "launches": att_passes,
+                                # the gathers' own rate: each CSR entry gathers one random
+                                # neighbour record, served as one 64-B line (PMC: ~0.8 lines
+                                # per entry at C4, 1.0 at C5)
+                                "gather_lines": {
+                                    "bytes_per_launch": 64 * att_entries,
+                                    "rate_GBs": (64 * att_entries / (att_ms * 1e-3) / 1e9
+                                                 if att_ms > 0 else 0.0),
+                                    "note": "model: one 64-B line per CSR entry; the measured "
+                                            "line count is in `traffic`"}},
         "level_rate": {"resident_ms": res_ms, "streamed_ms": str_ms},
         # this rank's streamed aggregates: plain symmetric sweeps / bands (a shorter
         # dependency chain) / whole row blocks
