@@ -52,6 +52,11 @@ constexpr int kHeavyDeg = 2048;
 constexpr int kTileRows = GE_TILE_ROWS;  // <= 128 (two-wave scan)
 constexpr int kTileCap = GE_TILE_CAP;    // entries per tile (multiple of kRowT); longer rows are heavy
 constexpr int kTileMinRows = 65536;  // fewer rows: medium / light classes
+// kSegStore: heavy rows of at least this many entries are "early" (launch_rows): their
+// segments and chains run first, beside the tiles, so that the longest chains do not
+// start after the last segment.  C4 level 0: 299 rows of 8 192-135 339 entries (12 261
+// segments); the other heavy rows have <= 6 224.
+constexpr int kChainEarly = 16 * kTileCap;
 
 struct RowClasses {
   const int* rows = nullptr;
@@ -63,6 +68,9 @@ struct RowClasses {
   const long long* hoff = nullptr;
   int seg_mode = 0;               // kSegBinade / kSegStore when nseg > 0
   int nheavy = 0, ntiles = 0, nmed = 0, nlight = 0, nseg = 0;
+  // kSegStore: heavy rows [0, nearly) (the longest: heavy rows are in descending
+  // degree order) and their segments [0, nseg_early) run first, on the side stream
+  int nearly = 0, nseg_early = 0;
   int tile_off = 0;  // where tile_ptr starts in the host array
   int seg_off = 0;   // where seg starts in the host array
   int grid() const { return nheavy + (nmed + 3) / 4 + (nlight + kRowT - 1) / kRowT; }
@@ -96,11 +104,16 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
   if (const char* e = std::getenv("GE_ROWS_HEAVY")) heavy = std::min(std::atoi(e), tiles ? kTileCap : 1 << 30);
   out.clear();
   if (heavy_deg) heavy_deg->clear();
+  // heavy rows longest first: their chains bound the pass (a row's sum does not depend
+  // on where it sits in the list)
+  std::vector<int> hq;
   for (size_t q = 0; q < ids.size(); ++q)
-    if (deg[q] > heavy) {
-      out.push_back(ids[q]);
-      if (heavy_deg) heavy_deg->push_back(deg[q]);
-    }
+    if (deg[q] > heavy) hq.push_back((int)q);
+  std::stable_sort(hq.begin(), hq.end(), [&](int x, int y) { return deg[x] > deg[y]; });
+  for (int q : hq) {
+    out.push_back(ids[q]);
+    if (heavy_deg) heavy_deg->push_back(deg[q]);
+  }
   rc.nheavy = (int)out.size();
   std::vector<int> tp;
   if (tiles) {
@@ -136,10 +149,10 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
   rc.seg_mode = segs ? seg_mode : kSegNone;
   rc.seg_off = (int)out.size();
   rc.nseg = 0;
+  rc.nearly = rc.nseg_early = 0;
   if (segs) {
     int h = 0;
-    for (size_t q = 0; q < ids.size(); ++q) {
-      if (deg[q] <= heavy) continue;
+    for (int q : hq) {
       for (int a = 0; a < deg[q]; a += kTileCap) {
         out.push_back(h);
         out.push_back(a);
@@ -147,6 +160,10 @@ inline void classify_rows(const std::vector<int>& ids, const std::vector<int>& d
         ++rc.nseg;
       }
       ++h;
+      if (seg_mode == kSegStore && deg[q] >= kChainEarly) {
+        rc.nearly = h;
+        rc.nseg_early = rc.nseg;
+      }
     }
   }
 }
@@ -574,10 +591,10 @@ __device__ __forceinline__ void segment_store(const RowClasses& L, const P& p, i
 // from HBM into LDS; then gravity and the update.
 constexpr int kStoreChunk = 512;  // terms per dimension per chunk
 template <int D, class P>
-__global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p) {
+__global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p, int h0 = 0) {
   __shared__ __attribute__((aligned(16))) double buf[2][D * kStoreChunk];
   const int lane = threadIdx.x;
-  const int h = blockIdx.x;
+  const int h = blockIdx.x + h0;
   typename P::State st;
   p.load(L.rows[h], st);
   const int deg = st.e1 - st.e0;
@@ -618,19 +635,21 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p) {
 
 // Tiles get their own kernel: without the heavy path's registers and LDS it
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
-// Block b + first: a tile (< ntiles) or a heavy-row segment after them; `first`
-// lets the segments run as their own launch (kSegStore, beside the tiles).
+// Block b + first: a tile (< ntiles) or heavy-row segment seg0 + (b - ntiles) after
+// them; `first` lets segments run as their own launch (kSegStore: the early rows'
+// segments on the side stream), `seg0` lets the tiles' launch take the later ones.
 
 template <int D, class P>
-__global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int first = 0) {
+__global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int first = 0,
+                                                          int seg0 = 0) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
   const int b = (int)blockIdx.x + first;
   if (b < L.ntiles)
     tile_rows<D>(L, p, b, lds);
   else if (L.seg_mode == kSegStore)
-    segment_store<D>(L, p, b - L.ntiles);
+    segment_store<D>(L, p, seg0 + b - L.ntiles);
   else
-    segment_rows<D>(L, p, b - L.ntiles, lds);
+    segment_rows<D>(L, p, seg0 + b - L.ntiles, lds);
 }
 
 // P: a row policy with
@@ -740,18 +759,31 @@ inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStre
   const int tgrid = rc.ntiles + rc.nseg;
   if (rc.nseg > 0 && rc.seg_mode == kSegStore && rc.ntiles > 0 &&
       !std::getenv("GE_ROWS_SERIAL")) {
-    // the heavy rows' chain (their terms stored by the segment blocks, then one
-    // dependent add per term) is independent of the tiles: segments + chains on the
-    // side stream, beside the tiles (C4: 2.16 + 1.43 ms one after the other)
-    rs.ensure();
-    GE_HIP(hipEventRecord(rs.fork, s));
-    GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg), dim3(kRowT), 0, rs.side, rc, p,
-                       rc.ntiles);
-    hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy), dim3(64), 0, rs.side, rc, p);
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles), dim3(kRowT), 0, s, rc, p, 0);
-    GE_HIP(hipEventRecord(rs.join, rs.side));
-    GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
+    // a heavy row's chain (its terms stored by its segment blocks, then one dependent
+    // add per term) is independent of the tiles.  The early rows (the longest chains)
+    // store their segments and run their chains on the side stream, beside the tiles;
+    // the tiles' launch then takes the other rows' segments, whose chains are short and
+    // follow it.  (Round 5: all segments then all chains on the side stream, C4 2.07 +
+    // 1.43 ms one after the other, the 135 339-entry row's chain starting last.)
+    const bool early = rc.nearly > 0;
+    if (early) {
+      rs.ensure();
+      GE_HIP(hipEventRecord(rs.fork, s));
+      GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+      hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg_early), dim3(kRowT), 0, rs.side,
+                         rc, p, rc.ntiles, 0);
+      hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nearly), dim3(64), 0, rs.side, rc, p,
+                         0);
+    }
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles + rc.nseg - rc.nseg_early),
+                       dim3(kRowT), 0, s, rc, p, 0, rc.nseg_early);
+    if (rc.nheavy > rc.nearly)
+      hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy - rc.nearly), dim3(64), 0, s,
+                         rc, p, rc.nearly);
+    if (early) {
+      GE_HIP(hipEventRecord(rs.join, rs.side));
+      GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
+    }
     return;
   }
   if (rc.nseg > 0) {  // heavy rows as segments, then their sums and finish

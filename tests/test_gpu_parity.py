@@ -547,6 +547,28 @@ def test_faml_streamed_row_slots(ctx, oracle, monkeypatch, R, U, tiles, segs, re
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("dim", [3, 2])
+def test_faml_early_heavy_row_chains(ctx, oracle, monkeypatch, dim):
+    """Heavy member rows of >= kChainEarly (8 192) entries (ge_rows.hpp launch_rows):
+    their segments and chains run on the side stream beside the tiles' launch, which
+    takes the other heavy rows' segments; the short chains follow it.  Two early rows
+    (~12 000 and ~9 000 entries) and a later heavy row (~5 000), tiles forced."""
+    monkeypatch.setenv("GE_ROWS_TILES", "1")
+    sizes = [12000, 3000, 2000, 300]
+    n = sum(sizes)
+    A = G.with_hubs(G.rmat(n, 8 * n, seed=23), [(5, 12000), (600, 9000), (40, 5000)], seed=dim)
+    deg = np.diff(A[0])
+    assert (deg >= 8192).sum() >= 2 and ((deg > 512) & (deg < 8192)).any()
+    PT = _block_partition(n, sizes, seed=9)
+    vA = ge.vertex_of(PT)
+    m = len(sizes)
+    cA = G.random_coords(m, dim, seed=m)
+    rA = np.random.RandomState(m).uniform(0.0, 0.6, m)
+    want = oracle.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=3, seed=29)
+    got = ctx.force_atlas_ml(A, PT, vA, cA, rA, dim, iterations=3, seed=29)
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("chain,dim,repel", [
     ("0", 3, 1.0), ("0", 3, 1.5), ("0", 3, 2.0 ** 70), ("1e9", 3, 1.0), ("", 3, 1.0),
     ("0", 2, 1.0), ("0", 4, 0.75), ("1e9", 4, 1.0)])
