@@ -212,8 +212,8 @@ def pmc_traffic_per_launch(kernel_prefix, workload):
     FETCH_SIZE reports half the bytes of a wide coalesced read -> bytes =
     (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  One "launch" is one pass of the matching
     kernels: the sum over every matching dispatch divided by the dispatch count of the
-    least frequent matching kernel (the row pass launches its tile kernel twice --
-    segments, tiles -- and its heavy-chain kernel once)."""
+    least frequent matching kernel (the row pass launches its tile kernel three times --
+    early rows' segments, the other segments, tiles -- and each heavy-chain kernel once)."""
     def read(pattern, counter):
         import csv
         for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", pattern)), reverse=True):

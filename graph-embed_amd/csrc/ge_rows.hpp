@@ -53,7 +53,7 @@ constexpr int kTileRows = GE_TILE_ROWS;  // <= 128 (two-wave scan)
 constexpr int kTileCap = GE_TILE_CAP;    // entries per tile (multiple of kRowT); longer rows are heavy
 constexpr int kTileMinRows = 65536;  // fewer rows: medium / light classes
 // kSegStore: heavy rows of at least this many entries are "early" (launch_rows): their
-// segments and chains run first, beside the tiles, so that the longest chains do not
+// segments and chains run first, on the side stream, so that the longest chains do not
 // start after the last segment.  C4 level 0: 299 rows of 8 192-135 339 entries (12 261
 // segments); the other heavy rows have <= 6 224.
 constexpr int kChainEarly = 16 * kTileCap;
@@ -196,8 +196,9 @@ __device__ __forceinline__ double lane_dim_value(const double (&acc)[D], int kd)
 // pipelined: the reads of the next 16 terms are issued before the adds of the
 // current 16, so the LDS latency is hidden behind the dependent add chain
 // (without it every 16 terms paid a full LDS round trip).
+template <int B = 16>  // terms per block
 __device__ __forceinline__ double lane_chain(double a, const double* p, int cnt) {
-  constexpr int B = 16, R = B / 2;  // terms per block, 16-byte reads per block
+  constexpr int R = B / 2;  // 16-byte reads per block
   const double2* q = reinterpret_cast<const double2*>(p);
   const int np = cnt / (2 * B);  // pairs of blocks: ping-pong without branches
   if (np > 0) {
@@ -587,12 +588,18 @@ __device__ __forceinline__ void segment_store(const RowClasses& L, const P& p, i
 }
 
 // kSegStore, phase B: one wave per heavy row adds the stored terms in order
-// (lane k: dimension k) while the whole wave streams the next chunk of them
-// from HBM into LDS; then gravity and the update.
+// (lane k: dimension k) while the whole wave loads the next chunk of them from
+// HBM into registers; then the chunk goes to LDS (one buffer: it is written after
+// the adds of the one before), and at the end gravity and the update.
 constexpr int kStoreChunk = 512;  // terms per dimension per chunk
-template <int D, class P>
+// CH: terms per dimension per chunk, B: lane_chain's block.  The early rows (long
+// chains) take 512 / 16; the others 256 / 8, which halves the registers and so
+// doubles the waves in flight: their launch is many short chains, bound by the
+// latency of each one's loads rather than by its adds.  (Round 5 kept two LDS
+// buffers of 512: 24 KB per one-wave block at D = 3 held a CU to 6 chain waves.)
+template <int D, class P, int CH = kStoreChunk, int B = 16>
 __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p, int h0 = 0) {
-  __shared__ __attribute__((aligned(16))) double buf[2][D * kStoreChunk];
+  __shared__ __attribute__((aligned(16))) double buf[D * CH];
   const int lane = threadIdx.x;
   const int h = blockIdx.x + h0;
   typename P::State st;
@@ -601,13 +608,13 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p, int 
   const double* in = L.hterm + L.hoff[h];
   const int kd = lane < D ? lane : D - 1;
   double a = lane_dim_value<D>(st.acc, kd);
-  constexpr int PER = D * kStoreChunk / 64;  // values per lane per chunk
+  constexpr int PER = D * CH / 64;  // values per lane per chunk
   double v[PER];
-  auto fetch = [&](int c0) {  // chunk [c0, c0 + kStoreChunk) of every dimension
+  auto fetch = [&](int c0) {  // chunk [c0, c0 + CH) of every dimension
 #pragma unroll
     for (int r = 0; r < PER; ++r) {
-      const int x = lane + 64 * r;  // dimension x / kStoreChunk, item x % kStoreChunk
-      const int k = x / kStoreChunk, l = c0 + x % kStoreChunk;
+      const int x = lane + 64 * r;  // dimension x / CH, item x % CH
+      const int k = x / CH, l = c0 + x % CH;
       v[r] = l < deg ? in[(size_t)k * deg + l] : 0.0;
     }
   };
@@ -617,16 +624,15 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p, int 
   };
   if (deg > 0) {
     fetch(0);
-    put(buf[0]);
+    put(buf);
   }
-  int c = 0;
-  for (int c0 = 0; c0 < deg; c0 += kStoreChunk, ++c) {
-    wave_lds_sync();  // chunk c is in buf[c & 1]
-    const bool more = c0 + kStoreChunk < deg;
-    if (more) fetch(c0 + kStoreChunk);  // in flight during the adds below
-    a = lane_chain(a, buf[c & 1] + kd * kStoreChunk, min(kStoreChunk, deg - c0));
-    wave_lds_sync();
-    if (more) put(buf[(c + 1) & 1]);
+  for (int c0 = 0; c0 < deg; c0 += CH) {
+    wave_lds_sync();  // the chunk at c0 is in buf
+    const bool more = c0 + CH < deg;
+    if (more) fetch(c0 + CH);  // in flight during the adds below
+    a = lane_chain<B>(a, buf + kd * CH, min(CH, deg - c0));
+    wave_lds_sync();  // every lane has read the chunk
+    if (more) put(buf);
   }
 #pragma unroll
   for (int k = 0; k < D; ++k) st.acc[k] = __shfl(a, k);
@@ -635,21 +641,20 @@ __global__ void __launch_bounds__(64) heavy_chain_kernel(RowClasses L, P p, int 
 
 // Tiles get their own kernel: without the heavy path's registers and LDS it
 // keeps several blocks per CU in flight (the pass is gather-latency bound).
-// Block b + first: a tile (< ntiles) or heavy-row segment seg0 + (b - ntiles) after
-// them; `first` lets segments run as their own launch (kSegStore: the early rows'
-// segments on the side stream), `seg0` lets the tiles' launch take the later ones.
+// Block b: tile tile0 + b (b < nt), else heavy-row segment seg0 + (b - nt): every
+// tile then every segment, or (kSegStore) the tiles alone / a range of segments alone.
 
 template <int D, class P>
-__global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int first = 0,
-                                                          int seg0 = 0) {
+__global__ void __launch_bounds__(kRowT) tile_rows_kernel(RowClasses L, P p, int tile0, int nt,
+                                                          int seg0) {
   __shared__ __attribute__((aligned(16))) char lds[RowsLds<D, P>::tile];
-  const int b = (int)blockIdx.x + first;
-  if (b < L.ntiles)
-    tile_rows<D>(L, p, b, lds);
+  const int b = (int)blockIdx.x;
+  if (b < nt)
+    tile_rows<D>(L, p, tile0 + b, lds);
   else if (L.seg_mode == kSegStore)
-    segment_store<D>(L, p, seg0 + b - L.ntiles);
+    segment_store<D>(L, p, seg0 + b - nt);
   else
-    segment_rows<D>(L, p, seg0 + b - L.ntiles, lds);
+    segment_rows<D>(L, p, seg0 + b - nt, lds);
 }
 
 // P: a row policy with
@@ -728,7 +733,7 @@ struct RowStreams {
     nheavy = rc.nheavy;
   }
   hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, mid = nullptr;
   RowStreams() = default;
   RowStreams(const RowStreams&) = delete;
   RowStreams& operator=(const RowStreams&) = delete;
@@ -739,12 +744,14 @@ struct RowStreams {
     }
     if (fork) (void)hipEventDestroy(fork);
     if (join) (void)hipEventDestroy(join);
+    if (mid) (void)hipEventDestroy(mid);
   }
   void ensure() {
     if (side) return;
     GE_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     GE_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
     GE_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+    GE_HIP(hipEventCreateWithFlags(&mid, hipEventDisableTiming));
   }
 };
 
@@ -761,33 +768,41 @@ inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStre
       !std::getenv("GE_ROWS_SERIAL")) {
     // a heavy row's chain (its terms stored by its segment blocks, then one dependent
     // add per term) is independent of the tiles.  The early rows (the longest chains)
-    // store their segments and run their chains on the side stream, beside the tiles;
-    // the tiles' launch then takes the other rows' segments, whose chains are short and
-    // follow it.  (Round 5: all segments then all chains on the side stream, C4 2.07 +
-    // 1.43 ms one after the other, the 135 339-entry row's chain starting last.)
-    const bool early = rc.nearly > 0;
-    if (early) {
-      rs.ensure();
-      GE_HIP(hipEventRecord(rs.fork, s));
-      GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+    // store their segments and run their chains on the side stream; the caller's
+    // stream stores the other heavy rows' segments and then runs the tiles, while the
+    // side stream, once those segments are stored, runs their (short) chains.  C4
+    // (profiles/r06/rows_timeline_c4.txt): early segments 0-0.2 ms, early chains to
+    // 1.2 ms; other segments to 1.2 ms, tiles to 2.6 ms beside the other chains
+    // (1.22-1.58 ms).  Round 5 stored all segments and then ran all chains on the side
+    // stream beside the tiles (2.07 + 1.43 ms: the 135 339-entry row's chain started
+    // last); DESIGN.md 5d has the variants measured.
+    const int nlate = rc.nseg - rc.nseg_early;
+    rs.ensure();
+    GE_HIP(hipEventRecord(rs.fork, s));
+    GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
+    if (rc.nearly > 0) {
       hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.nseg_early), dim3(kRowT), 0, rs.side,
-                         rc, p, rc.ntiles, 0);
+                         rc, p, 0, 0, 0);
       hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nearly), dim3(64), 0, rs.side, rc, p,
                          0);
     }
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles + rc.nseg - rc.nseg_early),
-                       dim3(kRowT), 0, s, rc, p, 0, rc.nseg_early);
-    if (rc.nheavy > rc.nearly)
-      hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy - rc.nearly), dim3(64), 0, s,
-                         rc, p, rc.nearly);
-    if (early) {
-      GE_HIP(hipEventRecord(rs.join, rs.side));
-      GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
+    if (nlate > 0) {
+      hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(nlate), dim3(kRowT), 0, s, rc, p, 0, 0,
+                         rc.nseg_early);
+      GE_HIP(hipEventRecord(rs.mid, s));
+      GE_HIP(hipStreamWaitEvent(rs.side, rs.mid, 0));
+      hipLaunchKernelGGL((heavy_chain_kernel<D, P, 256, 8>), dim3(rc.nheavy - rc.nearly), dim3(64),
+                         0, rs.side, rc, p, rc.nearly);
     }
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(rc.ntiles), dim3(kRowT), 0, s, rc, p, 0,
+                       rc.ntiles, 0);
+    GE_HIP(hipEventRecord(rs.join, rs.side));
+    GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
     return;
   }
   if (rc.nseg > 0) {  // heavy rows as segments, then their sums and finish
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0,
+                       rc.ntiles, 0);
     if (rc.seg_mode == kSegStore)
       hipLaunchKernelGGL((heavy_chain_kernel<D, P>), dim3(rc.nheavy), dim3(64), 0, s, rc, p);
     else
@@ -797,17 +812,20 @@ inline void launch_rows(const RowClasses& rc, const P& p, hipStream_t s, RowStre
   }
   if (rc.ntiles > 0 && rc.nheavy > 0 && std::getenv("GE_ROWS_SERIAL")) {  // tuning: no overlap
     hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.nheavy), dim3(kRowT), 0, s, rc, p);
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0,
+                       rc.ntiles, 0);
   } else if (rc.ntiles > 0 && rc.nheavy > 0) {
     rs.ensure();
     GE_HIP(hipEventRecord(rs.fork, s));
     GE_HIP(hipStreamWaitEvent(rs.side, rs.fork, 0));
     hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.nheavy), dim3(kRowT), 0, rs.side, rc, p);
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0,
+                       rc.ntiles, 0);
     GE_HIP(hipEventRecord(rs.join, rs.side));
     GE_HIP(hipStreamWaitEvent(s, rs.join, 0));
   } else if (rc.ntiles > 0) {
-    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0);
+    hipLaunchKernelGGL((tile_rows_kernel<D, P>), dim3(tgrid), dim3(kRowT), 0, s, rc, p, 0,
+                       rc.ntiles, 0);
   } else if (rc.grid() > 0) {
     hipLaunchKernelGGL((classed_rows_kernel<D, P>), dim3(rc.grid()), dim3(kRowT), 0, s, rc, p);
   }
