@@ -1037,30 +1037,36 @@ inline size_t packed_lds_bytes(int n, int D, int R) {
   return sizeof(double) * ((size_t)n * ((D + 1 <= 4) ? 4 : 8) + 2 * (size_t)R * D * kPackS);
 }
 
-// group_chain for the packed adder lane: the reads run GE_CHAIN_AHEAD batches (of 16
-// terms) ahead of the adds, so the LDS latency hides behind the dependent adds (3: n =
-// 998 18.2 us per iteration against 18.4 / 18.8 at 2 / 1).  The adder still takes ~20
-// cycles per add against 7 from registers and 11-12 from LDS in isolation
-// (scripts/micro/adder_chain.hip).  Same order of additions (slots >= cnt add +0.0).
+// group_chain for the packed adder lane: the first nb batches (of 16 terms) of a chunk,
+// the reads GE_CHAIN_AHEAD batches ahead of the adds, so the LDS latency hides behind
+// the dependent adds (3: n = 998 18.2 us per iteration against 18.4 / 18.8 at 2 / 1).
+// No per-lane count: the producers write every slot of a chunk, +0.0 past a row's own
+// terms, and adding +0.0 leaves a sum that starts at +0.0 unchanged (it is never -0.0),
+// so a lane adds the batches any lane of the block needs (nb, block-uniform) and skips
+// the rest.  Round 5 tested a count per lane and per batch (26 cycles per add against
+// 12 without, scripts/micro/adder_chain.hip) and added all six batches of every chunk.
 #ifndef GE_CHAIN_AHEAD
 #define GE_CHAIN_AHEAD 3
 #endif
 template <int G>
-__device__ __forceinline__ double chain_prefetch(double a, const double* p, int cnt) {
+__device__ __forceinline__ double chain_prefetch(double a, const double* p, int nb) {
   constexpr int B = 16, NB = G / B, P = GE_CHAIN_AHEAD, R = P + 1;
   static_assert(G % B == 0, "batches of 16");
   double v[R][B];
 #pragma unroll
-  for (int b = 0; b < P && b < NB; ++b)
+  for (int b = 0; b < P && b < NB; ++b) {
+    if (b >= nb) break;
 #pragma unroll
     for (int l = 0; l < B; l += 2) {
       const double2 x = *reinterpret_cast<const double2*>(p + b * B + l);
       v[b][l] = x.x;
       v[b][l + 1] = x.y;
     }
+  }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    if (b + P < NB) {
+    if (b >= nb) break;
+    if (b + P < NB && b + P < nb) {
 #pragma unroll
       for (int l = 0; l < B; l += 2) {
         const double2 x = *reinterpret_cast<const double2*>(p + (b + P) * B + l);
@@ -1068,13 +1074,8 @@ __device__ __forceinline__ double chain_prefetch(double a, const double* p, int 
         v[(b + P) % R][l + 1] = x.y;
       }
     }
-    if (cnt >= G) {
 #pragma unroll
-      for (int l = 0; l < B; ++l) a = a + v[b % R][l];
-    } else {
-#pragma unroll
-      for (int l = 0; l < B; ++l) a = a + ((b * B + l < cnt) ? v[b % R][l] : 0.0);
-    }
+    for (int l = 0; l < B; ++l) a = a + v[b % R][l];
   }
   return a;
 }
@@ -1168,7 +1169,6 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
   for (int r = 0; r < R; ++r) maxdeg = max(maxdeg, s_e[r][1] - s_e[r][0]);
   const int natt = (maxdeg + kPackC - 1) / kPackC;
   const int ntot = nrep + natt;  // the repulsion chunks, then the attraction chunks
-  const int adeg = adder ? s_e[ar][1] - s_e[ar][0] : 0;
   if (prod && ntot > 0) {
     if (nrep > 0) rep_chunk(0, tb);
     else att_chunk(0, tb);
@@ -1177,11 +1177,10 @@ __device__ __forceinline__ void packed_iteration(int blk, int n, int rb, int re,
   for (int ch = 0; ch < ntot; ++ch) {
     const double* cur = tb + (ch & 1) * BUF;
     if (tid < 64) {
-      if (adder) {
-        const int cnt = ch < nrep ? min(kPackC, n - ch * kPackC)
-                                  : min(kPackC, max(0, adeg - (ch - nrep) * kPackC));
-        if (cnt > 0) a = chain_prefetch<kPackC>(a, cur + (ar * D + ak) * kPackS, cnt);
-      }
+      // the largest count of the chunk over the block's rows (uniform)
+      const int cmax = ch < nrep ? min(kPackC, n - ch * kPackC)
+                                 : min(kPackC, maxdeg - (ch - nrep) * kPackC);
+      if (adder) a = chain_prefetch<kPackC>(a, cur + (ar * D + ak) * kPackS, (cmax + 15) >> 4);
     } else if (ch + 1 < ntot) {
       double* nxt = tb + ((ch + 1) & 1) * BUF;
       if (ch + 1 < nrep) rep_chunk(ch + 1, nxt);
@@ -1819,23 +1818,41 @@ bool launch_persistent(ge_fa_plan* pl, double* Xa, double* Xb, int iterations) {
     auto one = [&](auto RO, auto LI) {
       constexpr bool R1 = decltype(RO)::value, LIN = decltype(LI)::value;
       const bool pk = GC == 64 && packed_on;
-      // packed rows per block: 6 where blocks of 4 would outnumber the CUs (n = 1 068 at
-      // C4: 178 blocks of 6 against 267 of 4; GE_FA_PACK_ROWS=4|6 overrides, tuning)
-      int R = pk ? ((n + 3) / 4 > pl->cus ? 6 : 4) : 0;
-      if (const char* e = std::getenv("GE_FA_PACK_ROWS"); pk && e) R = std::atoi(e) == 6 ? 6 : 4;
+      // packed rows per block: 4, or 6 where the blocks of 4 would not all be resident
+      // at once.  Round 5 took 6 past one block of 4 per CU (C4's n = 1 068: 178 blocks
+      // of 6 against 267 of 4); since the adder skips the batches no row needs (round
+      // 6), 4 is faster at every size measured, 998-1 380 (16.1-16.6 against 16.9-17.1
+      // us per iteration on the C4-sized fixture, profiles/r06/coarse_rows_sweep.log).
+      // GE_FA_PACK_ROWS=4|6 overrides (tuning).
+      auto kernel_of = [&](int r) {
+        return !pk     ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>)
+               : r == 6 ? reinterpret_cast<const void*>(
+                              &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 6 : 0>)
+                        : reinterpret_cast<const void*>(
+                              &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 4 : 0>);
+      };
+      auto lds_of = [&](int r) {
+        return pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D, r))
+                  : grouped_lds_bytes(n, D);
+      };
+      auto occupancy = [&](int r) {
+        const void* f = kernel_of(r);
+        const size_t l = lds_of(r);
+        if (l > 65536)
+          GE_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l));
+        int o = 0;
+        GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, f, kGrpT, l));
+        return o;
+      };
+      int R = pk ? 4 : 0;
+      if (const char* e = std::getenv("GE_FA_PACK_ROWS"); pk && e)
+        R = std::atoi(e) == 6 ? 6 : 4;
+      else if (pk && (long long)((n + 3) / 4) > (long long)occupancy(4) * pl->cus)
+        R = 6;
       const int nbk = pk ? (n + R - 1) / R : nb;
-      size_t lds = pk ? std::max(grouped_lds_bytes(n, D), packed_lds_bytes(n, D, R))
-                      : grouped_lds_bytes(n, D);
-      const void* fn =
-          !pk    ? reinterpret_cast<const void*>(&fa_grouped_persistent<D, GC, R1, LIN>)
-          : R == 6 ? reinterpret_cast<const void*>(
-                         &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 6 : 0>)
-                   : reinterpret_cast<const void*>(
-                         &fa_grouped_persistent<D, GC, R1, LIN, GC == 64 ? 4 : 0>);
-      if (lds > 65536)
-        GE_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      int occ = 0;
-      GE_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kGrpT, lds));
+      const size_t lds = lds_of(R);
+      const void* fn = kernel_of(R);
+      const int occ = occupancy(R);
       if ((long long)nbk > (long long)occ * pl->cus) return;  // the whole grid resident
       fits = true;
       int dev = 0, khz = 0;

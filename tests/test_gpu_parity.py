@@ -273,8 +273,8 @@ def test_fa_persistent_small_level(ctx, oracle, monkeypatch, n, dim, grp, its):
     alternating buffers); odd and even counts, G lanes per row.  At 64 lanes per
     row the rows are packed (packed_iteration: one adder wave, three producer
     waves; ragged last block, rows of degree above one chunk); "nopack" keeps one
-    wave per row; "pack4" / "pack6" force 4 / 6 packed rows per block (6 is the
-    default once blocks of 4 would outnumber the CUs, n > 1024)."""
+    wave per row; "pack4" / "pack6" force 4 / 6 packed rows per block (4 is the
+    default; 6 only where the blocks of 4 would not all be resident)."""
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
     if grp == "nopack":
         monkeypatch.setenv("GE_FA_PACKED", "0")
@@ -332,7 +332,7 @@ def test_fa_coarsest_level_1e5_iterations(ctx, oracle):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("grp", ["0", "nopack", "16", "32", "pack4"])
+@pytest.mark.parametrize("grp", ["0", "nopack", "16", "32", "pack6"])
 def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     """The coarsest level at its production size and horizon: an R-MAT LCC coarsened
     twice by partition(A, 0.125) (n = 1067, integer weights, self-loops), seeded
@@ -342,8 +342,8 @@ def test_fa_coarsest_level_production_horizon(ctx, golden, monkeypatch, grp):
     monkeypatch.setenv("GE_PERSIST_REQUIRE", "1")
     if grp == "nopack":  # 64 lanes per row, one wave per row (grouped_iteration)
         monkeypatch.setenv("GE_FA_PACKED", "0")
-    elif grp == "pack4":  # 4 packed rows per block (n = 1067: the default is 6)
-        monkeypatch.setenv("GE_FA_PACK_ROWS", "4")
+    elif grp == "pack6":  # 6 packed rows per block (the default is 4 since round 6)
+        monkeypatch.setenv("GE_FA_PACK_ROWS", "6")
     elif grp != "0":
         monkeypatch.setenv("GE_GRP_G", grp)
     g = golden("fa_coarsest_1e5")
